@@ -1,0 +1,71 @@
+"""ctypes binding of ``libclasfv.so`` (C ABI declared in include/clasfv.h).
+
+There is no CPU fallback: if the library is missing or a call fails, a RuntimeError is raised.
+"""
+import ctypes
+import os
+
+from .build import LIB_PATH
+
+c_int, c_int64, c_void_p, c_char_p = ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_char_p
+_P = c_void_p
+
+# name -> (restype, argtypes); mirrors include/clasfv.h
+SIGNATURES = {
+    "clasfv_last_error": (c_char_p, []),
+    "clasfv_version": (c_int, []),
+    "clasfv_create": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
+    "clasfv_destroy": (c_int, [_P]),
+    "clasfv_param_count": (c_int, [_P]),
+    "clasfv_param_info": (c_int, [_P, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int), ctypes.POINTER(c_int64)]),
+    "clasfv_load_param": (c_int, [_P, c_char_p, _P, c_int64]),
+    "clasfv_finalize": (c_int, [_P]),
+    "clasfv_forward": (c_int, [_P, _P, c_int, c_int, c_int, c_int, _P, _P, _P]),
+    "clasfv_workspace_bytes": (c_int64, [_P]),
+    "clasfv_build_clips": (c_int, [_P, c_int, c_int, c_int, _P, c_int, c_int, _P, _P]),
+    "clasfv_pass_labels": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, _P]),
+    "clasfv_fuse_votes": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, _P, _P]),
+    "clasfv_warp": (c_int, [_P, c_int, c_int, c_int, c_int, _P, c_int64, c_int64, _P, _P]),
+    "clasfv_zeroone_normalize": (c_int, [_P, c_int64, _P]),
+}
+
+FUSE_MAJORITY, FUSE_SIMPLE = 0, 1
+_lib = None
+
+
+def lib_path():
+    return LIB_PATH
+
+
+def load():
+    """Load (building first if needed) and return the ctypes library."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        from .build import build
+        build()
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = load().clasfv_last_error()
+        raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+    return rc
+
+
+def stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr())

@@ -1,0 +1,58 @@
+"""Build ``libclasfv.so`` (all HIP kernels + the C ABI) for gfx950 with hipcc, in-tree.
+
+The shared library lands next to this file so it travels with the repository snapshot to the GPU
+box (a JIT cache under ~/.cache would not). Rebuilt only when a source is newer than the library.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+INCLUDE = os.path.join(REPO_DIR, "include")
+LIB_PATH = os.path.join(PKG_DIR, "libclasfv.so")
+SOURCES = ["engine.hip", "conv.hip", "decoder.hip", "plumbing.hip"]
+HEADERS = ["common.h", "plumbing.h"]
+ARCH = os.environ.get("CLASFV_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: the CLAS-FV engine needs ROCm's hipcc to build libclasfv.so")
+
+
+def _inputs():
+    files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    files.append(os.path.join(INCLUDE, "clasfv.h"))
+    return files
+
+
+def up_to_date():
+    if not os.path.exists(LIB_PATH):
+        return False
+    t = os.path.getmtime(LIB_PATH)
+    return all(os.path.getmtime(f) <= t for f in _inputs())
+
+
+def build(force=False, verbose=False):
+    """Compile the engine. Returns the library path."""
+    if not force and up_to_date():
+        return LIB_PATH
+    tmp = LIB_PATH + ".tmp"
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", INCLUDE,
+           "-o", tmp] + [os.path.join(CSRC, f) for f in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-6000:]}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,46 @@
+// Shared declarations of the CLAS-FV engine (internal; the public ABI is include/clasfv.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// One bias-free conv3d (BN folded into weights/bias) as an implicit GEMM over channels-last
+// activations: Y[m][n] = sum_k A[m][k] * W[n][k] (+bias[n], +res[m][n], relu).
+//   m = ((n*To + to)*Ho + ho)*Wo + wo            (output voxel)
+//   k = ((kt*KH + kh)*KW + kw)*Cin + c           (tap-major, channel-minor)
+struct ConvParams {
+  const float* x;     // [N][Ti][Hi][Wi][Cin]
+  const float* w;     // [Cout_alloc][Kp], zero padded
+  const float* bias;  // [Cout_alloc] or nullptr
+  const float* res;   // [M][Cout] or nullptr (may alias y)
+  float* y;           // [M][Cout]
+  int N, Ti, Hi, Wi, Cin;
+  int To, Ho, Wo, Cout;
+  int KT, KH, KW, st, sh, sw, pt, ph, pw;
+  int K, Kp, M, relu;
+};
+
+// Decoder tap: low-resolution projection P_i = (s1 * W_i) . f_i, channels-last with 64 channels.
+struct DecTap {
+  const float* p;
+  int T, H, W;
+  float st, sh, sw;  // align_corners=True source scales (in-1)/(out-1)
+};
+
+struct DecParams {
+  DecTap tap[4];      // (stem+layer1), layer2, layer3, layer4
+  const float* b1;    // [64]    comb_1 bias with BN1 folded
+  const float* w2;    // [64*64] comb_2 weight with BN2 folded, [n][k]
+  const float* b2;    // [64]
+  const float* wh;    // [8*64]  rows: seg0, seg1, mot0..mot3, 0, 0
+  const float* bh;    // [8]
+  float* seg;         // (N,2,T,H,W)
+  float* mot;         // (N,4,T,H,W)
+  int N, T, H, W;
+};
+
+// Launchers (stream-ordered, no synchronisation). Return hipError_t of the launch.
+hipError_t launch_conv(const ConvParams& p, int bn, hipStream_t s);
+hipError_t launch_decoder(const DecParams& p, hipStream_t s);
+hipError_t launch_pack_input(const float* x, float* y, int N, int T, int HW, hipStream_t s);

@@ -1,0 +1,237 @@
+// Fused full-resolution CLAS-FV decoder for gfx950.
+//
+// Reference (src/model/R2plus1D_18_MotionNet.py:39-71): five trilinear align_corners=True
+// upsamplings of the encoder taps to (T,H,W), torch.cat to 1024 channels (1.64 GB at 32x112x112),
+// conv 1x1x1 1024->64 + BN + ReLU, conv 64->64 + BN + ReLU, seg head 64->2, motion head 64->4 + tanh.
+//
+// Here: trilinear upsampling is linear and per channel, so comb_1(cat(up(f_i))) = sum_i up(W_i f_i).
+// The 1x1x1 projections P_i = (s1*W_i) f_i are computed at tap resolution by the conv kernel
+// (stem+layer1 share one resolution and are summed there), and this kernel, per output tile of one
+// frame x 8 rows x 16 cols:
+//   1. stages the 2 x rows x cols x 64-channel source windows of the four P tensors in LDS;
+//   2. interpolates them per voxel in registers (lane = voxel column, 16 channels per lane) and
+//      adds b1 -> ReLU -> h1 (never written to HBM);
+//   3. h2^T = W2 . h1^T on v_mfma_f32_16x16x4_f32: h1 is already the B operand in registers;
+//   4. bias + ReLU, then heads^T = Wh . h2^T on MFMA again: the 16x16 accumulator layout of step 3
+//      (rows = channels on lane groups, cols = voxels on lanes) is exactly the B-operand layout;
+//   5. writes seg logits and tanh(motion) in the reference (N,C,T,H,W) layout, 64-B coalesced.
+#include "common.h"
+
+namespace {
+
+constexpr int PIX = 68;  // floats per staged pixel: 64 channels + 4 pad (fewer LDS bank conflicts)
+constexpr int TILE_H = 8, TILE_W = 16;
+__constant__ const int kMaxRows[4] = {6, 4, 3, 3};
+__constant__ const int kMaxCols[4] = {10, 6, 4, 3};
+constexpr int kPixOff[5] = {0, 2 * 6 * 10, 2 * 6 * 10 + 2 * 4 * 6, 2 * 6 * 10 + 2 * 4 * 6 + 2 * 3 * 4,
+                            2 * 6 * 10 + 2 * 4 * 6 + 2 * 3 * 4 + 2 * 3 * 3};
+constexpr int STAGE_FLOATS = kPixOff[4] * PIX;
+
+struct Win {
+  int t0, t1, nf, r0, nr, c0, nc;
+  float lt0, lt1;
+};
+
+__device__ inline void src_index(float s, int dst, int in, int& i0, int& i1, float& l0, float& l1) {
+  const float f = s * (float)dst;
+  i0 = min((int)floorf(f), in - 1);
+  l1 = fminf(fmaxf(f - (float)i0, 0.f), 1.f);
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l0 = 1.f - l1;
+}
+
+__global__ __launch_bounds__(256) void decoder_kernel(DecParams p) {
+  extern __shared__ __align__(16) float smem[];
+  float* stage = smem;                                      // STAGE_FLOATS
+  f32x4* w2s = reinterpret_cast<f32x4*>(smem + STAGE_FLOATS);  // [16 k4][64 n] float4
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int q = lane >> 4, l16 = lane & 15;
+  const int tiles_w = p.W / TILE_W;
+  const int h0 = (blockIdx.x / tiles_w) * TILE_H, w0 = (blockIdx.x % tiles_w) * TILE_W;
+  const int t = blockIdx.y, n = blockIdx.z;
+
+  // W2 (64x64, [n][k]) -> LDS k4-major: w2s[kq*64 + n] = W2[n][4kq .. 4kq+3]
+  for (int e = tid; e < 16 * 64; e += 256) {
+    const int nn = e & 63, kq = e >> 6;
+    w2s[kq * 64 + nn] = *reinterpret_cast<const f32x4*>(p.w2 + nn * 64 + kq * 4);
+  }
+
+  // Source windows of the four taps.
+  Win win[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const DecTap& tp = p.tap[i];
+    Win w;
+    int a, b;
+    float la, lb;
+    src_index(tp.st, t, tp.T, a, b, la, lb);
+    w.t0 = a;
+    w.t1 = b;
+    w.lt0 = la;
+    w.lt1 = lb;
+    w.nf = (lb > 0.f && b != a) ? 2 : 1;
+    const int r0 = min((int)floorf(tp.sh * (float)h0), tp.H - 1);
+    const int r1 = min((int)floorf(tp.sh * (float)(h0 + TILE_H - 1)) + 1, tp.H - 1);
+    const int c0 = min((int)floorf(tp.sw * (float)w0), tp.W - 1);
+    const int c1 = min((int)floorf(tp.sw * (float)(w0 + TILE_W - 1)) + 1, tp.W - 1);
+    w.r0 = r0;
+    w.nr = min(r1 - r0 + 1, kMaxRows[i]);
+    w.c0 = c0;
+    w.nc = min(c1 - c0 + 1, kMaxCols[i]);
+    win[i] = w;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const DecTap& tp = p.tap[i];
+    const Win& w = win[i];
+    const int total = w.nf * w.nr * w.nc * 16;
+    float* dst = stage + kPixOff[i] * PIX;
+    for (int e = tid; e < total; e += 256) {
+      const int c4 = e & 15, px = e >> 4;
+      const int cc = px % w.nc, tmp = px / w.nc;
+      const int rr = tmp % w.nr, ff = tmp / w.nr;
+      const int tf = ff ? w.t1 : w.t0;
+      const size_t off = ((((size_t)n * tp.T + tf) * tp.H + (w.r0 + rr)) * tp.W + (w.c0 + cc)) * 64 + c4 * 4;
+      *reinterpret_cast<f32x4*>(dst + px * PIX + c4 * 4) = *reinterpret_cast<const f32x4*>(tp.p + off);
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. interpolation: lane = (voxel column l16, channel group q); h1[mt][4c + j] = ch 16c+4q+j
+  f32x4 h1[2][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b1 + 16 * c + 4 * q);
+    h1[0][c] = bb;
+    h1[1][c] = bb;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const DecTap& tp = p.tap[i];
+    const Win& w = win[i];
+    const float* src = stage + kPixOff[i] * PIX;
+    const int wc = w0 + l16;
+    int x0, x1;
+    float lx0, lx1;
+    src_index(tp.sw, wc, tp.W, x0, x1, lx0, lx1);
+    x0 -= w.c0;
+    x1 -= w.c0;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int hr = h0 + 2 * wid + mt;
+      int y0, y1;
+      float ly0, ly1;
+      src_index(tp.sh, hr, tp.H, y0, y1, ly0, ly1);
+      y0 -= w.r0;
+      y1 -= w.r0;
+      for (int f = 0; f < w.nf; ++f) {
+        const float wt = f ? w.lt1 : w.lt0;
+        const float* fb = src + f * w.nr * w.nc * PIX;
+        const float* p00 = fb + (y0 * w.nc + x0) * PIX + 4 * q;
+        const float* p01 = fb + (y0 * w.nc + x1) * PIX + 4 * q;
+        const float* p10 = fb + (y1 * w.nc + x0) * PIX + 4 * q;
+        const float* p11 = fb + (y1 * w.nc + x1) * PIX + 4 * q;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const f32x4 v00 = *reinterpret_cast<const f32x4*>(p00 + 16 * c);
+          const f32x4 v01 = *reinterpret_cast<const f32x4*>(p01 + 16 * c);
+          const f32x4 v10 = *reinterpret_cast<const f32x4*>(p10 + 16 * c);
+          const f32x4 v11 = *reinterpret_cast<const f32x4*>(p11 + 16 * c);
+          const f32x4 top = v00 * lx0 + v01 * lx1;
+          const f32x4 bot = v10 * lx0 + v11 * lx1;
+          h1[mt][c] += (top * ly0 + bot * ly1) * wt;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h1[mt][c][j] = fmaxf(h1[mt][c][j], 0.f);
+
+  // ---- 3. h2^T[n][v] = sum_k W2[n][k] h1[v][k]; MFMA j of lane group q covers k = 16c + 4q + j
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    f32x4 wa[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wa[c] = w2s[(c * 4 + q) * 64 + nt * 16 + l16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[c][j], h1[mt][c][j], acc[mt][nt], 0, 0, 0);
+  }
+  // acc[mt][nt][r] = h2^T[ch = 16nt + 4q + r][voxel l16]
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[mt][nt][r] = fmaxf(acc[mt][nt][r] + bb[r], 0.f);
+  }
+
+  // ---- 4. heads^T[co][v] = sum_k Wh[co][k] h2^T[k][v]; lane's B operand for (nt, r) is k = 16nt+4q+r
+  f32x4 wh[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) wh[nt] = *reinterpret_cast<const f32x4*>(p.wh + (l16 & 7) * 64 + 16 * nt + 4 * q);
+  if (l16 >= 8) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) wh[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  f32x4 out[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    out[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        out[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[mt][nt][r], out[mt], 0, 0, 0);
+  }
+
+  // ---- 5. out[mt][r] = head (4q + r) at voxel (h0 + 2*wid + mt, w0 + l16)
+  const size_t HW = (size_t)p.H * p.W;
+  const size_t TH = (size_t)p.T * HW;
+  if (q < 2) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const size_t pix = (size_t)t * HW + (size_t)(h0 + 2 * wid + mt) * p.W + (w0 + l16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 4 * q + r;
+        if (co >= 6) continue;
+        const float v = out[mt][r] + p.bh[co];
+        if (co < 2)
+          p.seg[((size_t)n * 2 + co) * TH + pix] = v;
+        else
+          p.mot[((size_t)n * 4 + (co - 2)) * TH + pix] = tanhf(v);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_decoder(const DecParams& p, hipStream_t s) {
+  dim3 grid((p.H / TILE_H) * (p.W / TILE_W), p.T, p.N);
+  const size_t lds = (size_t)STAGE_FLOATS * 4 + 16 * 64 * 16;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)decoder_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(decoder_kernel, grid, dim3(256), lds, s, p);
+  return hipGetLastError();
+}

@@ -1,0 +1,555 @@
+// CLAS-FV engine: network plan, weight folding, workspace arena and the C ABI (include/clasfv.h).
+//
+// Reference module: R2plus1D_18_MotionNet (src/model/R2plus1D_18_MotionNet.py:10-71) on top of
+// torchvision 0.6.0 r2plus1d_18. The 242 state-dict entries are accepted under the reference key
+// names (optionally "module."-prefixed, motion_segment.py:69-72); clasfv_finalize folds every
+// eval-mode BatchNorm into the preceding convolution, pads channel counts for the kernels
+// (45->48, 230->240, 460->480, 921->960) and uploads everything to HBM once.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "clasfv.h"
+#include "common.h"
+#include "plumbing.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) return fail(CLASFV_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+constexpr double kBnEps = 1e-5;
+
+struct Param {
+  std::string name;
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+  bool loaded = false;
+  int64_t numel() const {
+    int64_t n = 1;
+    for (auto d : shape) n *= d;
+    return n;
+  }
+};
+
+int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+int pad_channels(int c) {
+  if (c == 3) return 4;
+  int cp = round_up(c, 16);
+  if (cp % 64 != 0 && cp % 48 != 0) cp = round_up(cp, 48);
+  return cp;
+}
+
+enum Role { STEM_S, STEM_T, SP1, TP1, SP2, TP2, DS, PROJ };
+
+struct Conv {
+  Role role;
+  std::string w, bn;  // parameter name prefixes (".weight" / BN module)
+  int cin, cout, cin_p, cout_p;
+  int kt, kh, kw, st, sh, sw, pt, ph, pw;
+  int K, Kp, bn_tile, cout_alloc;
+  float* dw = nullptr;
+  float* db = nullptr;
+};
+
+Conv make_conv(Role role, const std::string& w, const std::string& bn, int cin, int cout, int kt, int kh, int kw,
+               int st, int sh, int sw, int pt, int ph, int pw) {
+  Conv c;
+  c.role = role;
+  c.w = w;
+  c.bn = bn;
+  c.cin = cin;
+  c.cout = cout;
+  c.cin_p = pad_channels(cin);
+  c.cout_p = pad_channels(cout);
+  c.kt = kt, c.kh = kh, c.kw = kw, c.st = st, c.sh = sh, c.sw = sw, c.pt = pt, c.ph = ph, c.pw = pw;
+  c.K = kt * kh * kw * c.cin_p;
+  c.Kp = round_up(c.K, 16);
+  c.bn_tile = (c.cout_p % 64 == 0) ? 64 : 48;
+  c.cout_alloc = round_up(c.cout_p, c.bn_tile);
+  return c;
+}
+
+int midplanes(int i, int o) { return (i * o * 27) / (i * 9 + 3 * o); }
+
+}  // namespace
+
+struct clasfv_engine {
+  int device = 0;
+  std::vector<Param> params;
+  std::unordered_map<std::string, int> index;
+  std::vector<Conv> convs;  // backbone, execution order
+  Conv proj[5];             // decoder projections (stem, layer1..4) -> 64 channels
+  float *b1 = nullptr, *w2 = nullptr, *b2 = nullptr, *wh = nullptr, *bh = nullptr;
+  bool ready = false;
+  // workspace arena
+  char* arena = nullptr;
+  size_t arena_bytes = 0;
+  float* part = nullptr;  // normaliser partials
+};
+
+namespace {
+
+void add_param(clasfv_engine* e, const std::string& name, std::vector<int64_t> shape) {
+  Param p;
+  p.name = name;
+  p.shape = std::move(shape);
+  e->index[name] = (int)e->params.size();
+  e->params.push_back(std::move(p));
+}
+
+void add_bn(clasfv_engine* e, const std::string& pre, int c) {
+  add_param(e, pre + ".weight", {c});
+  add_param(e, pre + ".bias", {c});
+  add_param(e, pre + ".running_mean", {c});
+  add_param(e, pre + ".running_var", {c});
+  add_param(e, pre + ".num_batches_tracked", {});
+}
+
+// Build the layer plan and the state-dict table in the reference's registration order.
+void build_plan(clasfv_engine* e) {
+  const std::string R = "r2plus1d_model.";
+  auto reg = [&](const Conv& c) {
+    add_param(e, c.w + ".weight", {c.cout, c.cin, c.kt, c.kh, c.kw});
+    add_bn(e, c.bn, c.cout);
+    e->convs.push_back(c);
+  };
+  reg(make_conv(STEM_S, R + "stem.0", R + "stem.1", 3, 45, 1, 7, 7, 1, 2, 2, 0, 3, 3));
+  reg(make_conv(STEM_T, R + "stem.3", R + "stem.4", 45, 64, 3, 1, 1, 1, 1, 1, 1, 0, 0));
+  int inplanes = 64;
+  const int planes_l[4] = {64, 128, 256, 512}, stride_l[4] = {1, 2, 2, 2};
+  for (int li = 0; li < 4; ++li) {
+    const int planes = planes_l[li], stride = stride_l[li];
+    for (int b = 0; b < 2; ++b) {
+      const int st = b == 0 ? stride : 1;
+      const int cin1 = b == 0 ? inplanes : planes;
+      const int mid = midplanes(cin1, planes);
+      const std::string pre = R + "layer" + std::to_string(li + 1) + "." + std::to_string(b) + ".";
+      reg(make_conv(SP1, pre + "conv1.0.0", pre + "conv1.0.1", cin1, mid, 1, 3, 3, 1, st, st, 0, 1, 1));
+      reg(make_conv(TP1, pre + "conv1.0.3", pre + "conv1.1", mid, planes, 3, 1, 1, st, 1, 1, 1, 0, 0));
+      reg(make_conv(SP2, pre + "conv2.0.0", pre + "conv2.0.1", planes, mid, 1, 3, 3, 1, 1, 1, 0, 1, 1));
+      reg(make_conv(TP2, pre + "conv2.0.3", pre + "conv2.1", mid, planes, 3, 1, 1, 1, 1, 1, 1, 0, 0));
+      if (b == 0 && (stride != 1 || inplanes != planes))
+        reg(make_conv(DS, pre + "downsample.0", pre + "downsample.1", inplanes, planes, 1, 1, 1, stride, stride,
+                      stride, 0, 0, 0));
+    }
+    inplanes = planes;
+  }
+  add_param(e, R + "fc.weight", {400, 512});
+  add_param(e, R + "fc.bias", {400});
+  add_param(e, "comb_1_layer.weight", {64, 1024, 1, 1, 1});
+  add_param(e, "comb_1_layer.bias", {64});
+  add_bn(e, "comb_batch_norm_1", 64);
+  add_param(e, "comb_2_layer.weight", {64, 64, 1, 1, 1});
+  add_param(e, "comb_2_layer.bias", {64});
+  add_bn(e, "comb_batch_norm_2", 64);
+  add_param(e, "motion_head.weight", {4, 64, 1, 1, 1});
+  add_param(e, "motion_head.bias", {4});
+  add_param(e, "segmentation_head.weight", {2, 64, 1, 1, 1});
+  add_param(e, "segmentation_head.bias", {2});
+  const int tap_c[5] = {64, 64, 128, 256, 512};
+  for (int i = 0; i < 5; ++i) e->proj[i] = make_conv(PROJ, "", "", tap_c[i], 64, 1, 1, 1, 1, 1, 1, 0, 0, 0);
+}
+
+const std::vector<float>& P(clasfv_engine* e, const std::string& n) { return e->params[e->index.at(n)].data; }
+
+void bn_scale_shift(clasfv_engine* e, const std::string& bn, int c, std::vector<double>& s, std::vector<double>& t) {
+  const auto& g = P(e, bn + ".weight");
+  const auto& b = P(e, bn + ".bias");
+  const auto& m = P(e, bn + ".running_mean");
+  const auto& v = P(e, bn + ".running_var");
+  s.resize(c);
+  t.resize(c);
+  for (int i = 0; i < c; ++i) {
+    s[i] = (double)g[i] / sqrt((double)v[i] + kBnEps);
+    t[i] = (double)b[i] - (double)m[i] * s[i];
+  }
+}
+
+int upload(const std::vector<float>& h, float** d) {
+  HIP_TRY(hipMalloc(d, h.size() * sizeof(float)));
+  HIP_TRY(hipMemcpy(*d, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+  return CLASFV_OK;
+}
+
+// Folded, padded [cout_alloc][Kp] weight image of one conv. `wsrc(o, c, tap)` returns the raw weight.
+template <class F>
+int upload_conv(Conv& c, F wsrc, const std::vector<double>& scale, const std::vector<double>& shift, bool has_bias) {
+  std::vector<float> w((size_t)c.cout_alloc * c.Kp, 0.f);
+  const int taps = c.kt * c.kh * c.kw;
+  for (int o = 0; o < c.cout; ++o)
+    for (int tap = 0; tap < taps; ++tap)
+      for (int ci = 0; ci < c.cin; ++ci)
+        w[(size_t)o * c.Kp + (size_t)tap * c.cin_p + ci] = (float)((double)wsrc(o, ci, tap) * scale[o]);
+  int rc = upload(w, &c.dw);
+  if (rc) return rc;
+  if (has_bias) {
+    std::vector<float> b(c.cout_alloc, 0.f);
+    for (int o = 0; o < c.cout; ++o) b[o] = (float)shift[o];
+    rc = upload(b, &c.db);
+  }
+  return rc;
+}
+
+struct Shape5 {
+  int n, t, h, w, c;
+  size_t numel() const { return (size_t)n * t * h * w * c; }
+};
+
+int run_conv(const Conv& c, const float* x, const Shape5& in, float* y, Shape5& out, const float* res, bool relu,
+             hipStream_t s) {
+  out.n = in.n;
+  out.t = (in.t + 2 * c.pt - c.kt) / c.st + 1;
+  out.h = (in.h + 2 * c.ph - c.kh) / c.sh + 1;
+  out.w = (in.w + 2 * c.pw - c.kw) / c.sw + 1;
+  out.c = c.cout_p;
+  if (in.c != c.cin_p) return fail(CLASFV_EINVAL, "internal: channel mismatch");
+  ConvParams p;
+  p.x = x;
+  p.w = c.dw;
+  p.bias = c.db;
+  p.res = res;
+  p.y = y;
+  p.N = in.n, p.Ti = in.t, p.Hi = in.h, p.Wi = in.w, p.Cin = in.c;
+  p.To = out.t, p.Ho = out.h, p.Wo = out.w, p.Cout = out.c;
+  p.KT = c.kt, p.KH = c.kh, p.KW = c.kw, p.st = c.st, p.sh = c.sh, p.sw = c.sw, p.pt = c.pt, p.ph = c.ph, p.pw = c.pw;
+  p.K = c.K, p.Kp = c.Kp;
+  p.M = out.n * out.t * out.h * out.w;
+  p.relu = relu ? 1 : 0;
+  HIP_TRY(launch_conv(p, c.bn_tile, s));
+  return CLASFV_OK;
+}
+
+// Workspace layout for one (N,T,H,W).
+struct Layout {
+  size_t off[32];
+  size_t total;
+};
+enum Buf { XIN, S0, X0, MID, TA, DSB, L1A, L1, L2A, L2, L3A, L3, L4A, L4, P01, PP2, PP3, PP4, NBUF };
+
+void make_layout(int N, int T, int H, int W, Layout& L) {
+  const size_t T1 = T, H2 = H / 2, W2 = W / 2;
+  size_t sz[NBUF];
+  sz[XIN] = (size_t)N * T * H * W * 4;
+  sz[S0] = (size_t)N * T1 * H2 * W2 * 48;
+  sz[X0] = (size_t)N * T1 * H2 * W2 * 64;
+  const size_t l1 = (size_t)N * T1 * H2 * W2 * 64;
+  const size_t l2 = (size_t)N * (T / 2) * (H / 4) * (W / 4) * 128;
+  const size_t l3 = (size_t)N * (T / 4) * (H / 8) * (W / 8) * 256;
+  const size_t l4 = (size_t)N * (T / 8) * (H / 16) * (W / 16) * 512;
+  size_t mid = (size_t)N * T1 * H2 * W2 * 144;
+  mid = std::max(mid, (size_t)N * T1 * (H / 4) * (W / 4) * 240);
+  mid = std::max(mid, (size_t)N * (T / 2) * (H / 8) * (W / 8) * 480);
+  mid = std::max(mid, (size_t)N * (T / 4) * (H / 16) * (W / 16) * 960);
+  sz[MID] = mid;
+  sz[TA] = std::max(std::max(l1, l2), std::max(l3, l4));
+  sz[DSB] = std::max(l2, std::max(l3, l4));
+  sz[L1A] = sz[L1] = l1;
+  sz[L2A] = sz[L2] = l2;
+  sz[L3A] = sz[L3] = l3;
+  sz[L4A] = sz[L4] = l4;
+  sz[P01] = (size_t)N * T1 * H2 * W2 * 64;
+  sz[PP2] = (size_t)N * (T / 2) * (H / 4) * (W / 4) * 64;
+  sz[PP3] = (size_t)N * (T / 4) * (H / 8) * (W / 8) * 64;
+  sz[PP4] = (size_t)N * (T / 8) * (H / 16) * (W / 16) * 64;
+  size_t o = 0;
+  for (int i = 0; i < NBUF; ++i) {
+    L.off[i] = o;
+    o += (sz[i] * sizeof(float) + 255) / 256 * 256;
+  }
+  L.total = o;
+}
+
+float tap_scale(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
+
+}  // namespace
+
+extern "C" {
+
+const char* clasfv_last_error(void) { return g_err.c_str(); }
+int clasfv_version(void) { return 1; }
+
+int clasfv_create(int device, clasfv_t* out) {
+  if (!out) return fail(CLASFV_EINVAL, "null out");
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(CLASFV_EINVAL, "bad device index");
+  auto* e = new clasfv_engine();
+  e->device = device;
+  build_plan(e);
+  *out = e;
+  return CLASFV_OK;
+}
+
+int clasfv_destroy(clasfv_t h) {
+  if (!h) return CLASFV_OK;
+  (void)hipSetDevice(h->device);
+  for (auto& c : h->convs) {
+    (void)hipFree(c.dw);
+    (void)hipFree(c.db);
+  }
+  for (auto& c : h->proj) (void)hipFree(c.dw);
+  (void)hipFree(h->b1);
+  (void)hipFree(h->w2);
+  (void)hipFree(h->b2);
+  (void)hipFree(h->wh);
+  (void)hipFree(h->bh);
+  (void)hipFree(h->arena);
+  (void)hipFree(h->part);
+  delete h;
+  return CLASFV_OK;
+}
+
+int clasfv_param_count(clasfv_t h) { return h ? (int)h->params.size() : CLASFV_EINVAL; }
+
+int clasfv_param_info(clasfv_t h, int i, const char** name, int* ndim, int64_t dims[5]) {
+  if (!h || i < 0 || i >= (int)h->params.size()) return fail(CLASFV_EINVAL, "bad param index");
+  const Param& p = h->params[i];
+  if (name) *name = p.name.c_str();
+  if (ndim) *ndim = (int)p.shape.size();
+  if (dims)
+    for (size_t d = 0; d < p.shape.size(); ++d) dims[d] = p.shape[d];
+  return CLASFV_OK;
+}
+
+int clasfv_load_param(clasfv_t h, const char* name, const float* data, int64_t numel) {
+  if (!h || !name) return fail(CLASFV_EINVAL, "null argument");
+  std::string n(name);
+  if (n.rfind("module.", 0) == 0) n = n.substr(7);
+  auto it = h->index.find(n);
+  if (it == h->index.end()) return fail(CLASFV_EINVAL, "unknown parameter: " + n);
+  Param& p = h->params[it->second];
+  if (n.size() > 20 && n.compare(n.size() - 20, 20, ".num_batches_tracked") == 0) {
+    p.loaded = true;
+    return CLASFV_OK;
+  }
+  if (numel != p.numel()) return fail(CLASFV_EINVAL, "size mismatch for " + n);
+  if (!data) return fail(CLASFV_EINVAL, "null data");
+  p.data.assign(data, data + numel);
+  p.loaded = true;
+  h->ready = false;
+  return CLASFV_OK;
+}
+
+int clasfv_finalize(clasfv_t h) {
+  if (!h) return fail(CLASFV_EINVAL, "null handle");
+  for (const auto& p : h->params)
+    if (!p.loaded && p.name.find(".fc.") == std::string::npos)
+      return fail(CLASFV_ENOTREADY, "parameter not loaded: " + p.name);
+  HIP_TRY(hipSetDevice(h->device));
+  std::vector<double> s, t;
+  for (auto& c : h->convs) {
+    (void)hipFree(c.dw);
+    (void)hipFree(c.db);
+    c.dw = c.db = nullptr;
+    bn_scale_shift(h, c.bn, c.cout, s, t);
+    const auto& w = P(h, c.w + ".weight");
+    const int taps = c.kt * c.kh * c.kw;
+    const int cin = c.cin;
+    int rc = upload_conv(
+        c, [&](int o, int ci, int tap) { return w[((size_t)o * cin + ci) * taps + tap]; }, s, t, true);
+    if (rc) return rc;
+  }
+  // comb_1 + BN1 folded, split per tap (concat order stem, layer1, layer2, layer3, layer4)
+  bn_scale_shift(h, "comb_batch_norm_1", 64, s, t);
+  const auto& w1 = P(h, "comb_1_layer.weight");
+  const auto& bias1 = P(h, "comb_1_layer.bias");
+  std::vector<double> zero(64, 0.0);
+  int off = 0;
+  for (int i = 0; i < 5; ++i) {
+    Conv& c = h->proj[i];
+    (void)hipFree(c.dw);
+    c.dw = nullptr;
+    const int o0 = off;
+    int rc = upload_conv(
+        c, [&](int o, int ci, int) { return w1[(size_t)o * 1024 + o0 + ci]; }, s, zero, false);
+    if (rc) return rc;
+    off += c.cin;
+  }
+  std::vector<float> b1(64);
+  for (int o = 0; o < 64; ++o) b1[o] = (float)(s[o] * (double)bias1[o] + t[o]);
+  bn_scale_shift(h, "comb_batch_norm_2", 64, s, t);
+  const auto& w2 = P(h, "comb_2_layer.weight");
+  const auto& bias2 = P(h, "comb_2_layer.bias");
+  std::vector<float> w2f(64 * 64), b2(64);
+  for (int o = 0; o < 64; ++o) {
+    for (int k = 0; k < 64; ++k) w2f[o * 64 + k] = (float)((double)w2[o * 64 + k] * s[o]);
+    b2[o] = (float)(s[o] * (double)bias2[o] + t[o]);
+  }
+  const auto& ws = P(h, "segmentation_head.weight");
+  const auto& bs = P(h, "segmentation_head.bias");
+  const auto& wm = P(h, "motion_head.weight");
+  const auto& bm = P(h, "motion_head.bias");
+  std::vector<float> whf(8 * 64, 0.f), bhf(8, 0.f);
+  for (int k = 0; k < 64; ++k) {
+    whf[0 * 64 + k] = ws[k];
+    whf[1 * 64 + k] = ws[64 + k];
+    for (int m = 0; m < 4; ++m) whf[(2 + m) * 64 + k] = wm[m * 64 + k];
+  }
+  bhf[0] = bs[0];
+  bhf[1] = bs[1];
+  for (int m = 0; m < 4; ++m) bhf[2 + m] = bm[m];
+  for (float** d : {&h->b1, &h->w2, &h->b2, &h->wh, &h->bh}) {
+    (void)hipFree(*d);
+    *d = nullptr;
+  }
+  int rc = upload(b1, &h->b1);
+  if (!rc) rc = upload(w2f, &h->w2);
+  if (!rc) rc = upload(b2, &h->b2);
+  if (!rc) rc = upload(whf, &h->wh);
+  if (!rc) rc = upload(bhf, &h->bh);
+  if (rc) return rc;
+  HIP_TRY(hipDeviceSynchronize());
+  h->ready = true;
+  return CLASFV_OK;
+}
+
+int64_t clasfv_workspace_bytes(clasfv_t h) { return h ? (int64_t)h->arena_bytes : 0; }
+
+int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float* seg, float* mot, void* stream) {
+  if (!h) return fail(CLASFV_EINVAL, "null handle");
+  if (!h->ready) return fail(CLASFV_ENOTREADY, "clasfv_finalize has not been called");
+  if (!x || !seg || !mot) return fail(CLASFV_EINVAL, "null tensor");
+  if (N < 1 || T < 8 || H < 16 || W < 16 || T % 8 || H % 16 || W % 16)
+    return fail(CLASFV_EBADSHAPE, "shape must satisfy T % 8 == 0, H % 16 == 0, W % 16 == 0 (got T=" +
+                                      std::to_string(T) + " H=" + std::to_string(H) + " W=" + std::to_string(W) + ")");
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipSetDevice(h->device));
+  Layout L;
+  make_layout(N, T, H, W, L);
+  if (L.total > h->arena_bytes) {
+    // The arena may still be in use by work queued earlier on any stream.
+    HIP_TRY(hipDeviceSynchronize());
+    (void)hipFree(h->arena);
+    h->arena = nullptr;
+    h->arena_bytes = 0;
+    HIP_TRY(hipMalloc(&h->arena, L.total));
+    h->arena_bytes = L.total;
+  }
+  auto buf = [&](int b) { return reinterpret_cast<float*>(h->arena + L.off[b]); };
+
+  HIP_TRY(launch_pack_input(x, buf(XIN), N, T, H * W, s));
+  Shape5 sx{N, T, H, W, 4}, s0, sx0;
+  int rc;
+  size_t ci = 0;
+  if ((rc = run_conv(h->convs[ci++], buf(XIN), sx, buf(S0), s0, nullptr, true, s))) return rc;
+  if ((rc = run_conv(h->convs[ci++], buf(S0), s0, buf(X0), sx0, nullptr, true, s))) return rc;
+  const int outs[4][2] = {{L1A, L1}, {L2A, L2}, {L3A, L3}, {L4A, L4}};
+  float* cur = buf(X0);
+  Shape5 cs = sx0, taps_shape[5];
+  float* taps[5];
+  taps[0] = cur;
+  taps_shape[0] = cs;
+  for (int li = 0; li < 4; ++li) {
+    for (int b = 0; b < 2; ++b) {
+      const Conv& sp1 = h->convs[ci++];
+      const Conv& tp1 = h->convs[ci++];
+      const Conv& sp2 = h->convs[ci++];
+      const Conv& tp2 = h->convs[ci++];
+      const Conv* ds = (ci < h->convs.size() && h->convs[ci].role == DS) ? &h->convs[ci++] : nullptr;
+      Shape5 sm, sa, sm2, so, sd;
+      if ((rc = run_conv(sp1, cur, cs, buf(MID), sm, nullptr, true, s))) return rc;
+      if ((rc = run_conv(tp1, buf(MID), sm, buf(TA), sa, nullptr, true, s))) return rc;
+      if ((rc = run_conv(sp2, buf(TA), sa, buf(MID), sm2, nullptr, true, s))) return rc;
+      const float* res = cur;
+      if (ds) {
+        if ((rc = run_conv(*ds, cur, cs, buf(DSB), sd, nullptr, false, s))) return rc;
+        res = buf(DSB);
+      }
+      float* out = buf(outs[li][b]);
+      if ((rc = run_conv(tp2, buf(MID), sm2, out, so, res, true, s))) return rc;
+      cur = out;
+      cs = so;
+    }
+    taps[li + 1] = cur;
+    taps_shape[li + 1] = cs;
+  }
+  // decoder projections at tap resolution: P01 = W0 f0 + W1 f1, P2..P4
+  Shape5 sp;
+  if ((rc = run_conv(h->proj[0], taps[0], taps_shape[0], buf(P01), sp, nullptr, false, s))) return rc;
+  if ((rc = run_conv(h->proj[1], taps[1], taps_shape[1], buf(P01), sp, buf(P01), false, s))) return rc;
+  Shape5 sp2, sp3, sp4;
+  if ((rc = run_conv(h->proj[2], taps[2], taps_shape[2], buf(PP2), sp2, nullptr, false, s))) return rc;
+  if ((rc = run_conv(h->proj[3], taps[3], taps_shape[3], buf(PP3), sp3, nullptr, false, s))) return rc;
+  if ((rc = run_conv(h->proj[4], taps[4], taps_shape[4], buf(PP4), sp4, nullptr, false, s))) return rc;
+
+  DecParams d;
+  const Shape5 tsh[4] = {sp, sp2, sp3, sp4};
+  const int tb[4] = {P01, PP2, PP3, PP4};
+  for (int i = 0; i < 4; ++i) {
+    d.tap[i].p = buf(tb[i]);
+    d.tap[i].T = tsh[i].t;
+    d.tap[i].H = tsh[i].h;
+    d.tap[i].W = tsh[i].w;
+    d.tap[i].st = tap_scale(tsh[i].t, T);
+    d.tap[i].sh = tap_scale(tsh[i].h, H);
+    d.tap[i].sw = tap_scale(tsh[i].w, W);
+  }
+  d.b1 = h->b1;
+  d.w2 = h->w2;
+  d.b2 = h->b2;
+  d.wh = h->wh;
+  d.bh = h->bh;
+  d.seg = seg;
+  d.mot = mot;
+  d.N = N, d.T = T, d.H = H, d.W = W;
+  HIP_TRY(launch_decoder(d, s));
+  return CLASFV_OK;
+}
+
+int clasfv_build_clips(const float* video, int T, int H, int W, const int32_t* table, int n, int interp, float* clips,
+                       void* stream) {
+  if (!video || !table || !clips || n < 0 || T < 1 || H < 1 || W < 1) return fail(CLASFV_EINVAL, "bad argument");
+  if (n == 0) return CLASFV_OK;
+  HIP_TRY(launch_build_clips(video, T, H * W, table, n, interp, clips, (hipStream_t)stream));
+  return CLASFV_OK;
+}
+
+int clasfv_pass_labels(const float* logits, int K, const int32_t* clip0, int T, int step, int H, int W, int interp,
+                       uint8_t* labels, void* stream) {
+  if (!logits || !clip0 || !labels || K < 1 || K > CLASFV_MAX_PASSES || T < 1 || step < 1)
+    return fail(CLASFV_EINVAL, "bad argument (K must be in [1, 64])");
+  HIP_TRY(launch_pass_labels(logits, K, clip0, T, step, H * W, interp, labels, (hipStream_t)stream));
+  return CLASFV_OK;
+}
+
+int clasfv_fuse_votes(const uint8_t* labels, int K, int T, int step, int H, int W, int method, uint8_t* fused,
+                      void* stream) {
+  if (!labels || !fused || K < 1 || K > 32 || T < 1 || step < 1 || T - (step - 1) < 1)
+    return fail(CLASFV_EINVAL, "bad argument (K must be in [1, 32])");
+  if (method != CLASFV_FUSE_MAJORITY && method != CLASFV_FUSE_SIMPLE) return fail(CLASFV_EINVAL, "unknown method");
+  HIP_TRY(launch_fuse_votes(labels, K, T, step, H * W, method, fused, (hipStream_t)stream));
+  return CLASFV_OK;
+}
+
+int clasfv_warp(const float* img, int N, int C, int H, int W, const float* motion, int64_t m_sn, int64_t m_sc,
+                float* out, void* stream) {
+  if (!img || !motion || !out || N < 1 || C < 1 || H < 1 || W < 1) return fail(CLASFV_EINVAL, "bad argument");
+  HIP_TRY(launch_warp(img, N, C, H, W, motion, m_sn, m_sc, out, (hipStream_t)stream));
+  return CLASFV_OK;
+}
+
+int clasfv_zeroone_normalize(float* video, int64_t n, void* stream) {
+  if (!video || n < 1) return fail(CLASFV_EINVAL, "bad argument");
+  static thread_local float* part = nullptr;  // per-thread partials buffer (3 x 512 x 2 floats)
+  if (!part) HIP_TRY(hipMalloc(&part, sizeof(float) * zeroone_partials_floats()));
+  HIP_TRY(launch_zeroone_normalize(video, n, part, (hipStream_t)stream));
+  return CLASFV_OK;
+}
+
+}  // extern "C"

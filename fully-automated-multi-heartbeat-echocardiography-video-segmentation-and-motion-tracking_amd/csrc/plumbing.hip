@@ -1,0 +1,379 @@
+// Memory-bound per-video kernels of the CLAS-FV clip pipeline (gfx950).
+//
+//   build_clips        divide_to_consecutive_clips        src/fuse_utils.py:16-33
+//   pass_labels        softmax -> temporal resample -> argmax   src/fuse_utils.py:53-80
+//   fuse_votes         per-frame label fusion            src/fuse_utils.py:82-100
+//   warp               generate_2dmotion_field + grid_sample   src/transform_utils.py:14-34
+//   zeroone_normalize  zeroone_normalizer                src/echonet_dataset.py:38-50
+//
+// Interpolation arithmetic follows PyTorch's CPU upsample kernel bit for bit (checked against
+// F.interpolate in tests): scale = (float)in/out, src = fma(scale, dst + 0.5, -0.5) clamped at 0,
+// value = fma(x[i0], l0, x[i1] * l1).
+#include <float.h>
+
+#include "common.h"
+#include "plumbing.h"
+
+namespace {
+
+__device__ inline int round_half_even_div32(int t) {
+  const int q = t >> 5, r = t & 31;
+  if (r > 16) return q + 1;
+  if (r < 16) return q;
+  return q + (q & 1);
+}
+
+struct Lin {
+  int i0, i1;
+  float l0, l1;
+};
+
+// align_corners=False source index for output index dst of a t_in -> t_out resampling.
+__device__ inline Lin lin_ac_false(int t_in, int t_out, int dst) {
+  Lin r;
+  const float scale = (float)t_in / (float)t_out;
+  float src = fmaf(scale, (float)dst + 0.5f, -0.5f);
+  src = fmaxf(src, 0.f);
+  r.i0 = min((int)floorf(src), t_in - 1);
+  r.l1 = fminf(fmaxf(src - (float)r.i0, 0.f), 1.f);
+  r.i1 = r.i0 + (r.i0 < t_in - 1 ? 1 : 0);
+  r.l0 = 1.f - r.l1;
+  return r;
+}
+
+__device__ inline float lerp_t(float a, float b, float l0, float l1) { return fmaf(a, l0, __fmul_rn(b, l1)); }
+
+// ---- build_clips ------------------------------------------------------------------------------
+__global__ void build_clips_kernel(const float* __restrict__ video, int T, int HW, const int32_t* __restrict__ table,
+                                   int interp, float* __restrict__ clips) {
+  const int clip = blockIdx.z, fr = blockIdx.y;  // fr in [0, 3*32)
+  const int c = fr >> 5, f = fr & 31;
+  const int shift = table[2 * clip], j0 = table[2 * clip + 1];
+  const int tk = T - shift;
+  const int tf = j0 + f;  // frame index in the (resampled) shifted video
+  const int tc = 32 * round_half_even_div32(tk);
+  const float* vc = video + (size_t)c * T * HW;
+  float* out = clips + (((size_t)clip * 3 + c) * 32 + f) * HW;
+  const bool resample = interp && (tk & 31) && tk != tc;
+  Lin L = {0, 0, 1.f, 0.f};
+  if (resample) L = lin_ac_false(tk, tc, tf);
+  const float* a = vc + (size_t)(shift + (resample ? L.i0 : tf)) * HW;
+  const float* b = vc + (size_t)(shift + (resample ? L.i1 : tf)) * HW;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += gridDim.x * blockDim.x)
+    out[i] = resample ? lerp_t(a[i], b[i], L.l0, L.l1) : a[i];
+}
+
+// ---- pass_labels ------------------------------------------------------------------------------
+struct PassTable {
+  int clip0[CLASFV_MAX_PASSES];
+};
+
+__device__ inline void softmax2(float x0, float x1, float& p0, float& p1) {
+  const float m = fmaxf(x0, x1);
+  const float e0 = expf(x0 - m), e1 = expf(x1 - m);
+  const float s = e0 + e1;
+  p0 = e0 / s;
+  p1 = e1 / s;
+}
+
+__global__ void pass_labels_kernel(const float* __restrict__ logits, PassTable tab, int T, int step, int HW,
+                                   int interp, uint8_t* __restrict__ labels) {
+  const int k = blockIdx.z, f = blockIdx.y;
+  const int tk = T - k * step;
+  if (f >= tk) return;
+  const int tc = 32 * round_half_even_div32(tk);
+  const bool resample = interp && (tk & 31) && tk != tc;
+  Lin L = {f, f, 1.f, 0.f};
+  if (resample) L = lin_ac_false(tc, tk, f);
+  const size_t clip_stride = (size_t)2 * 32 * HW;
+  const float* base = logits + (size_t)tab.clip0[k] * clip_stride;
+  const float* a = base + (size_t)(L.i0 >> 5) * clip_stride + (size_t)(L.i0 & 31) * HW;
+  const float* b = base + (size_t)(L.i1 >> 5) * clip_stride + (size_t)(L.i1 & 31) * HW;
+  const size_t cs = (size_t)32 * HW;  // class stride inside a clip
+  uint8_t* out = labels + ((size_t)k * T + f) * HW;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += gridDim.x * blockDim.x) {
+    float pa0, pa1;
+    softmax2(a[i], a[i + cs], pa0, pa1);
+    float q0 = pa0, q1 = pa1;
+    if (resample) {
+      float pb0, pb1;
+      softmax2(b[i], b[i + cs], pb0, pb1);
+      q0 = lerp_t(pa0, pb0, L.l0, L.l1);
+      q1 = lerp_t(pa1, pb1, L.l0, L.l1);
+    }
+    out[i] = q1 > q0 ? 1 : 0;  // np.argmax: first maximum wins ties
+  }
+}
+
+// ---- fuse_votes: majority ----------------------------------------------------------------------
+// Output frame o: o == 0 -> frame 0 of pass 0; o >= 1 -> frame i = o + step - 1.
+__device__ inline int n_votes(int i, int K, int step) {
+  int nv = 0;
+  const int kmax = min(i, K);
+  for (int idx = 0; idx < kmax; ++idx) {
+    if (i - idx * step < 0) break;
+    ++nv;
+  }
+  return nv;
+}
+
+__global__ void fuse_majority_kernel(const uint8_t* __restrict__ labels, int K, int T, int step, int HW,
+                                     uint8_t* __restrict__ fused) {
+  const int o = blockIdx.y;
+  const int i = o == 0 ? 0 : o + step - 1;
+  const int nv = o == 0 ? 1 : n_votes(i, K, step);
+  uint8_t* out = fused + (size_t)o * HW;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
+    int ones = 0;
+    for (int idx = 0; idx < nv; ++idx) ones += labels[((size_t)idx * T + (i - idx * step)) * HW + p];
+    out[p] = (nv == 1) ? (uint8_t)ones : (uint8_t)(2 * ones > nv ? 1 : 0);
+  }
+}
+
+// ---- fuse_votes: SIMPLE (one workgroup per output frame) --------------------------------------
+// Selective and iterative method for performance level estimation (Langerak et al. 2010) in the
+// BraTS-toolkit form: per label (1 then 0), weighted majority of the binarised candidates with
+// weights (dice(candidate, estimate) + 1)^2, drop candidates below 0.05 * max weight, stop when the
+// estimate's voxel count moves by < 25. PARITY UNPINNED: LabelFusion's source is not available.
+constexpr int SIMPLE_THREADS = 256;
+
+__device__ inline double block_sum(double v, double* red) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  double s = 0;
+  for (int w = 0; w < SIMPLE_THREADS / 64; ++w) s += red[w];
+  return s;
+}
+
+__global__ __launch_bounds__(SIMPLE_THREADS) void fuse_simple_kernel(const uint8_t* __restrict__ labels, int K, int T,
+                                                                      int step, int HW, uint8_t* __restrict__ fused) {
+  extern __shared__ uint8_t est[];  // HW bytes: current estimate
+  __shared__ double red[SIMPLE_THREADS / 64];
+  __shared__ double wts[CLASFV_MAX_PASSES];
+  const int o = blockIdx.x;
+  const int i = o == 0 ? 0 : o + step - 1;
+  const int nv = o == 0 ? 1 : n_votes(i, K, step);
+  uint8_t* out = fused + (size_t)o * HW;
+  auto vote = [&](int idx, int p) -> int { return labels[((size_t)idx * T + (i - idx * step)) * HW + p]; };
+  if (nv == 1) {
+    for (int p = threadIdx.x; p < HW; p += SIMPLE_THREADS) out[p] = (uint8_t)vote(0, p);
+    return;
+  }
+  for (int p = threadIdx.x; p < HW; p += SIMPLE_THREADS) out[p] = 0;
+  for (int lab = 1; lab >= 0; --lab) {
+    unsigned keep = (nv >= 32) ? 0xffffffffu : ((1u << nv) - 1u);
+    for (int idx = 0; idx < nv; ++idx) wts[idx] = 1.0;
+    __syncthreads();
+    // initial estimate: unweighted majority, ties -> off
+    double cnt = 0;
+    for (int p = threadIdx.x; p < HW; p += SIMPLE_THREADS) {
+      double on = 0, off = 0;
+      for (int idx = 0; idx < nv; ++idx) {
+        const bool c = vote(idx, p) == lab;
+        on += c ? 1.0 : 0.0;
+        off += c ? 0.0 : 1.0;
+      }
+      est[p] = on > off;
+      cnt += est[p];
+    }
+    double conv = block_sum(cnt, red);
+    for (int it = 0; it < 25; ++it) {
+      // dice of every kept candidate against the estimate
+      double esum = conv;
+      double mx = 0;
+      for (int idx = 0; idx < nv; ++idx) {
+        if (!(keep >> idx & 1u)) continue;
+        double inter = 0, csum = 0;
+        for (int p = threadIdx.x; p < HW; p += SIMPLE_THREADS) {
+          const bool c = vote(idx, p) == lab;
+          csum += c;
+          inter += (c && est[p]);
+        }
+        inter = block_sum(inter, red);
+        csum = block_sum(csum, red);
+        const double s = csum + esum;
+        const double d = (s == 0) ? 1.0 : 2.0 * inter / s;
+        const double w = (d + 1.0) * (d + 1.0);
+        if (threadIdx.x == 0) wts[idx] = w;
+        mx = fmax(mx, w);
+      }
+      __syncthreads();
+      for (int idx = 0; idx < nv; ++idx)
+        if ((keep >> idx & 1u) && !(wts[idx] > 0.05 * mx)) keep &= ~(1u << idx);
+      cnt = 0;
+      for (int p = threadIdx.x; p < HW; p += SIMPLE_THREADS) {
+        double on = 0, off = 0;
+        for (int idx = 0; idx < nv; ++idx) {
+          if (!(keep >> idx & 1u)) continue;
+          const bool c = vote(idx, p) == lab;
+          if (c)
+            on += wts[idx];
+          else
+            off += wts[idx];
+        }
+        est[p] = on > off;
+        cnt += est[p];
+      }
+      const double nsum = block_sum(cnt, red);
+      const bool stop = fabs(conv - nsum) < 25.0;
+      conv = nsum;
+      if (stop) break;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < HW; p += SIMPLE_THREADS)
+      if (est[p]) out[p] = (uint8_t)lab;
+    __syncthreads();
+  }
+}
+
+// ---- warp ------------------------------------------------------------------------------------
+// torch.linspace(-1, 1, n) on the CPU: step = 2/(n-1); first half start + step*i, second half
+// end - step*(n-1-i).
+__device__ inline float linspace_pm1(int i, int n) {
+  if (n == 1) return -1.f;
+  const float step = 2.0f / (float)(n - 1);
+  return (i < n / 2) ? (-1.f + step * (float)i) : (1.f - step * (float)(n - 1 - i));
+}
+
+__global__ void warp_kernel(const float* __restrict__ img, int N, int C, int H, int W, const float* __restrict__ motion,
+                            int64_t m_sn, int64_t m_sc, float* __restrict__ out) {
+  const size_t HW = (size_t)H * W;
+  const size_t total = (size_t)N * HW;
+  for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < total; g += (size_t)gridDim.x * blockDim.x) {
+    const int n = (int)(g / HW);
+    const int pix = (int)(g - (size_t)n * HW);
+    const int i = pix / W, j = pix - (pix / W) * W;
+    const float* mp = motion + n * m_sn + pix;
+    const float gx = linspace_pm1(j, W) + mp[0];
+    const float gy = linspace_pm1(i, H) + mp[m_sc];
+    // grid_sampler_compute_source_index: unnormalise (align_corners=False), border clip
+    float ix = __fdiv_rn(__fsub_rn(__fmul_rn(__fadd_rn(gx, 1.f), (float)W), 1.f), 2.f);
+    float iy = __fdiv_rn(__fsub_rn(__fmul_rn(__fadd_rn(gy, 1.f), (float)H), 1.f), 2.f);
+    ix = fminf((float)(W - 1), fmaxf(ix, 0.f));
+    iy = fminf((float)(H - 1), fmaxf(iy, 0.f));
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const int x0 = (int)fx0, y0 = (int)fy0, x1 = x0 + 1, y1 = y0 + 1;
+    const float wnw = __fmul_rn(fx0 + 1.f - ix, fy0 + 1.f - iy);
+    const float wne = __fmul_rn(ix - fx0, fy0 + 1.f - iy);
+    const float wsw = __fmul_rn(fx0 + 1.f - ix, iy - fy0);
+    const float wse = __fmul_rn(ix - fx0, iy - fy0);
+    const bool in_x1 = x1 < W, in_y1 = y1 < H;
+    for (int c = 0; c < C; ++c) {
+      const float* src = img + ((size_t)n * C + c) * HW;
+      float v = __fmul_rn(src[y0 * W + x0], wnw);
+      if (in_x1) v = __fadd_rn(v, __fmul_rn(src[y0 * W + x1], wne));
+      if (in_y1) v = __fadd_rn(v, __fmul_rn(src[y1 * W + x0], wsw));
+      if (in_x1 && in_y1) v = __fadd_rn(v, __fmul_rn(src[y1 * W + x1], wse));
+      out[((size_t)n * C + c) * HW + pix] = v;
+    }
+  }
+}
+
+// ---- zeroone_normalize -------------------------------------------------------------------------
+constexpr int RED_THREADS = 256, RED_BLOCKS = 512;
+
+__global__ void minmax_partial_kernel(const float* __restrict__ v, int64_t n, float* __restrict__ part) {
+  const int c = blockIdx.y;
+  const float* x = v + (size_t)c * n;
+  float lo = FLT_MAX, hi = -FLT_MAX;
+  for (int64_t i = blockIdx.x * (int64_t)RED_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * RED_THREADS) {
+    lo = fminf(lo, x[i]);
+    hi = fmaxf(hi, x[i]);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fminf(lo, __shfl_xor(lo, off, 64));
+    hi = fmaxf(hi, __shfl_xor(hi, off, 64));
+  }
+  __shared__ float slo[RED_THREADS / 64], shi[RED_THREADS / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    slo[wid] = lo;
+    shi[wid] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < RED_THREADS / 64; ++w) {
+      lo = fminf(lo, slo[w]);
+      hi = fmaxf(hi, shi[w]);
+    }
+    part[(c * gridDim.x + blockIdx.x) * 2] = lo;
+    part[(c * gridDim.x + blockIdx.x) * 2 + 1] = hi;
+  }
+}
+
+__global__ void normalize_kernel(float* __restrict__ v, int64_t n, const float* __restrict__ part, int nparts) {
+  const int c = blockIdx.y;
+  __shared__ float s_lo, s_den;
+  if (threadIdx.x == 0) {
+    float lo = FLT_MAX, hi = -FLT_MAX;
+    for (int b = 0; b < nparts; ++b) {
+      lo = fminf(lo, part[(c * nparts + b) * 2]);
+      hi = fmaxf(hi, part[(c * nparts + b) * 2 + 1]);
+    }
+    s_lo = lo;
+    s_den = __fsub_rn(hi, lo);  // == max over the channel of (x - min): subtraction is monotone
+  }
+  __syncthreads();
+  const float lo = s_lo, den = s_den;
+  float* x = v + (size_t)c * n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = __fdiv_rn(__fsub_rn(x[i], lo), den);
+}
+
+inline int blocks_for(size_t n, int per_block, int cap) {
+  size_t b = (n + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  return (int)(b > (size_t)cap ? cap : b);
+}
+
+}  // namespace
+
+hipError_t launch_build_clips(const float* video, int T, int HW, const int32_t* table, int n, int interp, float* clips,
+                              hipStream_t s) {
+  dim3 grid(blocks_for(HW, 256, 64), 3 * 32, n);
+  hipLaunchKernelGGL(build_clips_kernel, grid, dim3(256), 0, s, video, T, HW, table, interp, clips);
+  return hipGetLastError();
+}
+
+hipError_t launch_pass_labels(const float* logits, int K, const int32_t* clip0, int T, int step, int HW, int interp,
+                              uint8_t* labels, hipStream_t s) {
+  PassTable tab;
+  for (int k = 0; k < K; ++k) tab.clip0[k] = clip0[k];
+  dim3 grid(blocks_for(HW, 256, 64), T, K);
+  hipLaunchKernelGGL(pass_labels_kernel, grid, dim3(256), 0, s, logits, tab, T, step, HW, interp, labels);
+  return hipGetLastError();
+}
+
+hipError_t launch_fuse_votes(const uint8_t* labels, int K, int T, int step, int HW, int method, uint8_t* fused,
+                             hipStream_t s) {
+  const int tout = T - (step - 1);
+  if (method == 1) {
+    hipLaunchKernelGGL(fuse_simple_kernel, dim3(tout), dim3(SIMPLE_THREADS), HW, s, labels, K, T, step, HW, fused);
+  } else {
+    dim3 grid(blocks_for(HW, 256, 64), tout);
+    hipLaunchKernelGGL(fuse_majority_kernel, grid, dim3(256), 0, s, labels, K, T, step, HW, fused);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_warp(const float* img, int N, int C, int H, int W, const float* motion, int64_t m_sn, int64_t m_sc,
+                       float* out, hipStream_t s) {
+  const size_t total = (size_t)N * H * W;
+  hipLaunchKernelGGL(warp_kernel, dim3(blocks_for(total, 256, 8192)), dim3(256), 0, s, img, N, C, H, W, motion, m_sn,
+                     m_sc, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_zeroone_normalize(float* v, int64_t n, float* part, hipStream_t s) {
+  const int nb = blocks_for((size_t)n, RED_THREADS * 4, RED_BLOCKS);
+  hipLaunchKernelGGL(minmax_partial_kernel, dim3(nb, 3), dim3(RED_THREADS), 0, s, v, n, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(normalize_kernel, dim3(blocks_for((size_t)n, 1024, 2048), 3), dim3(256), 0, s, v, n, part, nb);
+  return hipGetLastError();
+}
+
+int zeroone_partials_floats() { return 3 * RED_BLOCKS * 2; }

@@ -1,0 +1,86 @@
+"""Clip-wise sharding of a batch of videos across ranks (one process per GPU).
+
+Every 32-frame clip of every temporally shifted pass of every video is independent
+(src/fuse_utils.py:45-61), so the global clip list is partitioned into contiguous blocks, one per
+rank; each rank runs the encoder-decoder on its block only, and one all-gather of the per-clip
+segmentation logits (2 x 32 x H x W fp32 per clip) over RCCL/xGMI gives every rank every clip
+before fusion. Fusion is then split by video (video v is fused by rank v % world). The result is
+bit-identical to the 1-GPU run because the per-clip computation is identical; only placement moves.
+"""
+import torch
+import torch.distributed as dist
+
+from . import fuse_utils as FU
+
+
+def shard_bounds(n, rank, world):
+    """Contiguous block [lo, hi) of n items for rank; sizes differ by at most one."""
+    q, r = divmod(n, world)
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def global_clip_plan(video_lengths, num_clips, step, interpolate_last=True):
+    """Per video: (K, table, clip0) and the global offset of its first clip."""
+    plans, off = [], 0
+    for t in video_lengths:
+        k = FU.clamp_num_clips(t, num_clips, step)
+        if k == 0:
+            raise IndexError("list index out of range")
+        table, clip0 = FU.clip_table(t, k, step, interpolate_last)
+        plans.append({"T": t, "K": k, "table": table, "clip0": clip0, "offset": off, "n": len(table)})
+        off += len(table)
+    return plans, off
+
+
+def all_gather_clips(local, n_total, rank, world, group=None):
+    """Gather per-clip tensors (n_local, ...) from every rank into (n_total, ...) in global order.
+    Blocks are padded to the largest shard so one all_gather_into_tensor moves everything."""
+    if world == 1:
+        return local
+    sizes = [shard_bounds(n_total, r, world) for r in range(world)]
+    mx = max(hi - lo for lo, hi in sizes)
+    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    if dist.get_backend(group) == "gloo":  # CPU test path: gloo has no all_gather_into_tensor
+        bufs = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(bufs, pad, group=group)
+        out = torch.cat(bufs)
+    else:
+        out = torch.empty((world * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out, pad, group=group)
+    parts = [out[r * mx: r * mx + (hi - lo)] for r, (lo, hi) in enumerate(sizes)]
+    return torch.cat(parts)
+
+
+def segment_videos_sharded(videos_dev, model, num_clips=5, step=1, fuse_method="simple", interpolate_last=True,
+                           rank=0, world=1, batch_size=None, clip_fn=None):
+    """Fuse a batch of device videos (each (3,T,H,W)) with clips sharded over ranks.
+
+    Returns {video index: fused (T',H,W) uint8 device tensor} for the videos this rank owns
+    (v % world == rank). ``clip_fn(clips) -> logits`` overrides the model call (tests)."""
+    plans, n_total = global_clip_plan([v.shape[1] for v in videos_dev], num_clips, step, interpolate_last)
+    lo, hi = shard_bounds(n_total, rank, world)
+    # build this rank's clips: per video, the overlap of its clip range with [lo, hi)
+    mine = []
+    for vi, p in enumerate(plans):
+        a, b = max(lo, p["offset"]), min(hi, p["offset"] + p["n"])
+        if a < b:
+            tab = p["table"][a - p["offset"]: b - p["offset"]]
+            mine.append(FU.build_clips(videos_dev[vi], tab, interpolate_last))
+    h, w = videos_dev[0].shape[-2:]
+    dev = videos_dev[0].device
+    if mine:
+        clips = torch.cat(mine) if len(mine) > 1 else mine[0]
+        logits = clip_fn(clips) if clip_fn else FU.run_model(model, clips, batch_size)
+    else:
+        logits = torch.empty((0, 2, FU.CLIP, h, w), device=dev, dtype=torch.float32)
+    logits = all_gather_clips(logits.contiguous(), n_total, rank, world)
+    out = {}
+    for vi, p in enumerate(plans):
+        if vi % world != rank:
+            continue
+        lg = logits[p["offset"]: p["offset"] + p["n"]]
+        labels = FU.pass_labels(lg, p["clip0"], p["T"], step, interpolate_last)
+        out[vi] = FU.fuse_votes(labels, step, fuse_method)
+    return out

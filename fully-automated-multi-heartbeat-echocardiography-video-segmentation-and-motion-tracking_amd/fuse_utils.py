@@ -1,0 +1,159 @@
+"""Drop-in clip plumbing and label fusion (src/fuse_utils.py:16-100) on the HIP engine.
+
+``segment_a_video_with_fusion(video, model, interpolate_last=True, step=1, num_clips=10,
+fuse_method="simple", class_list=[0, 1])`` returns the same (T', 112, 112) int64 label video as the
+reference, but every clip of every temporally shifted pass is built on the GPU
+(``clasfv_build_clips``), run through the model in batches instead of one batch-1 forward per clip
+(src/fuse_utils.py:53-61), and softmax -> temporal re-interpolation -> argmax -> per-frame fusion
+stay in HBM (``clasfv_pass_labels``, ``clasfv_fuse_votes``); only the final uint8 mask crosses PCIe.
+
+Reference behaviour kept: banker's rounding of the clip count (:22,29), the K clamp and its
+"Video is too short" message (:38-42), IndexError when K == 0 (:82, e.g. T == 32), frames 1..step-1
+dropped for step > 1 (:85), passes with different clip counts (numpy 1.19 ragged arrays, :50).
+Fusion: ``majority`` (= ``majorityvoting``/``mv``/``itkvoting``; ties -> background) and ``simple``
+(SIMPLE, Langerak 2010). LabelFusion itself is not available, so ``simple`` is parity-unpinned.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+
+FUSE_METHODS = {"majority": _lib.FUSE_MAJORITY, "majorityvoting": _lib.FUSE_MAJORITY, "mv": _lib.FUSE_MAJORITY,
+                "itkvoting": _lib.FUSE_MAJORITY, "voting": _lib.FUSE_MAJORITY, "simple": _lib.FUSE_SIMPLE}
+CLIP = 32
+DEFAULT_BATCH = 32
+
+
+def n_clips(t, clip_length=CLIP):
+    """Number of clips of a t-frame video: round(t / 32) with numpy's half-to-even rounding."""
+    return int(np.round(t / clip_length))
+
+
+def clamp_num_clips(t, num_clips, step):
+    """src/fuse_utils.py:38-42."""
+    if t < CLIP + num_clips * step:
+        num_clips = (t - CLIP) // step
+    if num_clips < 0:
+        print("Video is too short")
+        num_clips = 1
+    return num_clips
+
+
+def clip_table(t, num_passes, step, interpolate_last=True):
+    """[(shift, first_frame)] for every clip of every shifted pass, pass-major; and per-pass offsets."""
+    table, clip0 = [], []
+    for k in range(num_passes):
+        shift = k * step
+        tk = t - shift
+        nk = n_clips(tk)
+        if tk % CLIP != 0 and not interpolate_last and nk * CLIP > tk:
+            raise ValueError("all the input array dimensions except for the concatenation axis must match exactly")
+        if nk == 0:
+            raise ValueError(f"pass {k}: {tk} frames give no 32-frame clip")
+        clip0.append(len(table))
+        table.extend((shift, CLIP * j) for j in range(nk))
+    return table, clip0
+
+
+def _device_of(model):
+    eng = getattr(model, "engine", None)
+    if eng is not None:
+        return eng.device
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def to_device_video(video, device):
+    v = torch.as_tensor(np.asarray(video, np.float32) if not torch.is_tensor(video) else video)
+    return v.to(device, torch.float32).contiguous()
+
+
+def build_clips(video_dev, table, interpolate_last=True):
+    """(n,3,32,H,W) clips on the device for a [(shift, first_frame)] table."""
+    _, t, h, w = video_dev.shape
+    tab = torch.tensor(np.asarray(table, np.int32).reshape(-1), device=video_dev.device)
+    clips = torch.empty((len(table), 3, CLIP, h, w), device=video_dev.device, dtype=torch.float32)
+    lib = _lib.load()
+    _lib.check(lib.clasfv_build_clips(_lib.ptr(video_dev), t, h, w, _lib.ptr(tab), len(table), int(bool(interpolate_last)),
+                                      _lib.ptr(clips), _lib.stream_ptr()), "clasfv_build_clips")
+    return clips
+
+
+def divide_to_consecutive_clips(video, clip_length=CLIP, interpolate_last=False):
+    """src/fuse_utils.py:16-33. Returns a float32 device tensor (n,3,32,H,W)."""
+    if clip_length != CLIP:
+        raise ValueError("the engine uses 32-frame clips")
+    dev = torch.device("cuda", torch.cuda.current_device())
+    v = to_device_video(video, dev)
+    table, _ = clip_table(v.shape[1], 1, 1, interpolate_last)
+    return build_clips(v, table, interpolate_last)
+
+
+def run_model(model, clips, batch_size=None):
+    """Segmentation logits (n,2,32,H,W) of every clip; the motion output is discarded as in the
+    reference (src/fuse_utils.py:59)."""
+    n = clips.shape[0]
+    if batch_size is None:
+        batch_size = DEFAULT_BATCH if hasattr(model, "engine") else 1
+    outs = []
+    for s in range(0, n, batch_size):
+        seg, _ = model(clips[s:s + batch_size])
+        outs.append(seg.to(clips.device, torch.float32))
+    return torch.cat(outs) if len(outs) > 1 else outs[0].contiguous()
+
+
+def fuse_votes(labels, step, fuse_method="simple"):
+    k, t, h, w = labels.shape
+    method = FUSE_METHODS.get(fuse_method.lower())
+    if method is None:
+        raise NotImplementedError(f"fuse_method {fuse_method!r}: supported {sorted(FUSE_METHODS)}")
+    fused = torch.empty((t - (step - 1), h, w), device=labels.device, dtype=torch.uint8)
+    lib = _lib.load()
+    _lib.check(lib.clasfv_fuse_votes(_lib.ptr(labels), k, t, step, h, w, method, _lib.ptr(fused), _lib.stream_ptr()),
+               "clasfv_fuse_votes")
+    return fused
+
+
+def ctypes_int32_array(vals):
+    """Host int32 array for the ABI; returns (pointer, owner) -- keep the owner alive for the call."""
+    import ctypes
+    arr = (ctypes.c_int32 * max(1, len(vals)))(*vals)
+    return ctypes.cast(arr, ctypes.c_void_p), arr
+
+
+def segment_a_video_with_fusion_device(video, model, interpolate_last=True, step=1, num_clips=10, fuse_method="simple",
+                                       class_list=(0, 1), batch_size=None):
+    """Same as segment_a_video_with_fusion but returns the fused (T',H,W) uint8 mask on the device."""
+    if list(class_list) != [0, 1]:
+        raise ValueError("the engine fuses the two CLAS-FV classes [0, 1]")
+    dev = _device_of(model)
+    v = to_device_video(video, dev)
+    t = v.shape[1]
+    k = clamp_num_clips(t, num_clips, step)
+    if k == 0:
+        raise IndexError("list index out of range")  # src/fuse_utils.py:82 with no pass
+    table, clip0 = clip_table(t, k, step, interpolate_last)
+    clips = build_clips(v, table, interpolate_last)
+    logits = run_model(model, clips, batch_size)
+    labels = pass_labels(logits, clip0, t, step, interpolate_last)
+    return fuse_votes(labels, step, fuse_method)
+
+
+def pass_labels(logits, clip0, t, step, interpolate_last=True):
+    """(K,T,H,W) uint8 labels of the K shifted passes (softmax -> resample -> argmax)."""
+    k = len(clip0)
+    h, w = logits.shape[-2:]
+    labels = torch.empty((k, t, h, w), device=logits.device, dtype=torch.uint8)
+    ptr, keep = ctypes_int32_array(clip0)
+    lib = _lib.load()
+    _lib.check(lib.clasfv_pass_labels(_lib.ptr(logits), k, ptr, t, step, h, w, int(bool(interpolate_last)),
+                                      _lib.ptr(labels), _lib.stream_ptr()), "clasfv_pass_labels")
+    del keep
+    return labels
+
+
+def segment_a_video_with_fusion(video, model, interpolate_last=True, step=1, num_clips=10, fuse_method="simple",
+                                class_list=[0, 1], batch_size=None):
+    """src/fuse_utils.py:36-100 -> numpy int64 (T', H, W)."""
+    fused = segment_a_video_with_fusion_device(video, model, interpolate_last, step, num_clips, fuse_method, class_list,
+                                               batch_size)
+    return fused.to(torch.int64).cpu().numpy()

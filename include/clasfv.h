@@ -1,0 +1,101 @@
+/*
+ * clasfv.h -- C ABI of the MI355X-native CLAS-FV engine (libclasfv.so, gfx950).
+ *
+ * Drop-in boundary for the reference hot path (yc015/fully-automated-multi-heartbeat-echocardiography-
+ * video-segmentation-and-motion-tracking @ /root/reference):
+ *   model forward      R2plus1D_18_MotionNet.forward(x) -> (seg, motion)
+ *                        src/model/R2plus1D_18_MotionNet.py:26-71
+ *   checkpoint load    model.load_state_dict(torch.load(path)["model"])    motion_segment.py:69-72
+ *   clip plumbing      divide_to_consecutive_clips / segment_a_video_with_fusion
+ *                        src/fuse_utils.py:16-100
+ *   motion warp        generate_2dmotion_field + F.grid_sample(border, align_corners=False)
+ *                        src/transform_utils.py:14-34, src/visualization_utils.py:128
+ *   normaliser         zeroone_normalizer                                  src/echonet_dataset.py:38-50
+ *
+ * Conventions
+ *   - Plain C types only. Tensors are dense row-major fp32 (labels: uint8) in the reference's
+ *     layouts (N,C,T,H,W). Pointers marked _dev are device (HBM) pointers owned by the caller;
+ *     the library owns weights and its workspace.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream). All launches are
+ *     stream-ordered and asynchronous; no call synchronises the device except clasfv_finalize.
+ *   - Every function returns CLASFV_OK (0) or a negative error code; clasfv_last_error() returns
+ *     a thread-local message for the last failure. A handle is not re-entrant: calls on one handle
+ *     must be serialised by the caller (one handle per device per process).
+ */
+#ifndef CLASFV_H
+#define CLASFV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  CLASFV_OK = 0,
+  CLASFV_EINVAL = -1,     /* bad argument / unknown parameter name */
+  CLASFV_EBADSHAPE = -2,  /* shape not supported: T % 8, H % 16, W % 16 must be 0 */
+  CLASFV_ENOTREADY = -3,  /* forward before clasfv_finalize / missing parameters */
+  CLASFV_EHIP = -4,       /* HIP runtime error (message in clasfv_last_error) */
+  CLASFV_ENOMEM = -5
+};
+
+enum { CLASFV_FUSE_MAJORITY = 0, CLASFV_FUSE_SIMPLE = 1 };
+
+typedef struct clasfv_engine* clasfv_t;
+
+const char* clasfv_last_error(void);
+int clasfv_version(void);
+
+/* ---- model: replaces R2plus1D_18_MotionNet.__init__/load_state_dict/forward ------------------ */
+int clasfv_create(int device, clasfv_t* out);
+int clasfv_destroy(clasfv_t h);
+/* Number / name / shape of the 242 state-dict entries the engine accepts (reference key names,
+ * e.g. "r2plus1d_model.stem.0.weight"); shape is written to dims[0..*ndim). */
+int clasfv_param_count(clasfv_t h);
+int clasfv_param_info(clasfv_t h, int i, const char** name, int* ndim, int64_t dims[5]);
+/* Copy one state-dict entry from host memory. A "module." prefix (nn.DataParallel checkpoints,
+ * motion_segment.py:69) is accepted. num_batches_tracked entries are accepted and ignored. */
+int clasfv_load_param(clasfv_t h, const char* name, const float* host_data, int64_t numel);
+/* Fold eval-mode BatchNorm into the convolutions, pad channels for the kernels, upload to HBM. */
+int clasfv_finalize(clasfv_t h);
+/* seg_dev (N,2,T,H,W) logits and motion_dev (N,4,T,H,W) tanh outputs from x_dev (N,3,T,H,W). */
+int clasfv_forward(clasfv_t h, const float* x_dev, int N, int T, int H, int W, float* seg_dev,
+                   float* motion_dev, void* stream);
+/* Bytes of library workspace currently held (activation arena; grows to the largest N*T*H*W seen). */
+int64_t clasfv_workspace_bytes(clasfv_t h);
+
+/* ---- clip plumbing: replaces src/fuse_utils.py:16-100 ----------------------------------------- */
+/* Build n clips (n,3,32,H,W) from the normalised video (3,T,H,W). Clip i is frames
+ * [table[2i+1], table[2i+1]+32) of the temporally shifted video video[:, table[2i]:], resampled
+ * to 32*round(T_k/32) frames (align_corners=False, as F.interpolate) when interpolate != 0 and
+ * T_k % 32 != 0. table_dev is a device int32 array of 2n entries. */
+int clasfv_build_clips(const float* video_dev, int T, int H, int W, const int32_t* table_dev, int n,
+                       int interpolate, float* clips_dev, void* stream);
+/* For each shifted pass k < K: softmax over the 2 classes of the pass's clips' logits
+ * (logits_dev + pass_clip0[k] clips, each (2,32,H,W)), resample to T_k = T - k*step frames
+ * (align_corners=False) when T_k % 32 != 0 and interpolate != 0, argmax -> labels_dev[k][0..T_k)
+ * (labels_dev is (K,T,H,W) uint8). pass_clip0 is a host array of K ints. */
+int clasfv_pass_labels(const float* logits_dev, int K, const int32_t* pass_clip0, int T, int step, int H,
+                       int W, int interpolate, uint8_t* labels_dev, void* stream);
+/* Per-frame label fusion over the K shifted passes (fuse_utils.py:82-100). Output (T',H,W) uint8
+ * with T' = T - (step - 1). method: CLASFV_FUSE_MAJORITY or CLASFV_FUSE_SIMPLE. */
+int clasfv_fuse_votes(const uint8_t* labels_dev, int K, int T, int step, int H, int W, int method,
+                      uint8_t* fused_dev, void* stream);
+
+/* ---- motion warp (src/transform_utils.py:14-34 + grid_sample) ------------------------------------ */
+/* out (N,C,H,W) = bilinear sample of img at (linspace_W[j] + motion[n,0,i,j],
+ * linspace_H[i] + motion[n,1,i,j]), border padding, align_corners=False. motion is (N,2,H,W) with
+ * arbitrary element strides for n and the channel (so a slice motion[:, 0:2, t] of (N,4,T,H,W) can
+ * be passed directly): element (n,c,i,j) at motion_dev[n*m_sn + c*m_sc + i*W + j]. */
+int clasfv_warp(const float* img_dev, int N, int C, int H, int W, const float* motion_dev, int64_t m_sn,
+                int64_t m_sc, float* out_dev, void* stream);
+
+/* ---- preprocessing (src/echonet_dataset.py:38-50) ------------------------------------------------ */
+/* In place: per channel c of video (3, n_per_channel) subtract the channel min, divide by the max. */
+int clasfv_zeroone_normalize(float* video_dev, int64_t n_per_channel, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLASFV_H */

@@ -1,0 +1,197 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and the reference goldens.
+
+Tolerances: the forward is fp32 with a different summation order than cuDNN/mkldnn (implicit GEMM,
+folded BatchNorm, decoder commuted to project-then-interpolate), so raw logits are compared with an
+absolute tolerance and the derived masks with the north_star bar Dice delta <= 1e-3. Plumbing
+kernels (clip building, resample, argmax, voting, normaliser) are compared bit for bit.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fuse_ref, r2plus1d_ref, warp_ref
+from tests.conftest import golden, unpack_labels
+from tests.golden.fake_model import fake_model
+
+pytestmark = pytest.mark.gpu
+
+DICE_TOL = 1e-3
+
+
+def dice_delta(a, b):
+    from clasfv_amd.echo import categorical_dice
+    return 1.0 - categorical_dice(np.asarray(a), np.asarray(b), 1)
+
+
+@pytest.fixture(scope="module")
+def model():
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    return R2plus1D_18_MotionNet(pretrained=False)
+
+
+def test_native_library_is_loaded(model):
+    import clasfv_amd._lib as L
+    with open("/proc/self/maps") as f:
+        assert L.lib_path() in f.read()
+
+
+def test_forward_small_vs_reference_golden(model):
+    g = golden("model_forward.npz")
+    seg, mot = model(torch.from_numpy(g["x_small"]))
+    seg, mot = seg.cpu().numpy(), mot.cpu().numpy()
+    np.testing.assert_allclose(seg, g["seg_small"], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(mot, g["mot_small"], rtol=0, atol=1e-5)
+    ref_lab = g["seg_small"][:, 1] > g["seg_small"][:, 0]
+    assert dice_delta(seg[:, 1] > seg[:, 0], ref_lab) <= DICE_TOL
+
+
+def test_forward_full_clip_vs_reference_golden(model):
+    import clasfv_amd.synthetic as S
+    g = golden("model_forward.npz")
+    v = fuse_ref.zeroone_normalizer(S.echo_video(int(g["big_T"]), seed=int(g["big_video_seed"])))
+    s = int(g["big_start"])
+    seg, mot = model(torch.from_numpy(np.ascontiguousarray(v[None, :, s:s + 32])))
+    seg, mot = seg.cpu().numpy(), mot.cpu().numpy()
+    lab = (seg[0, 1] > seg[0, 0]).ravel()
+    ref = np.unpackbits(g["big_label_bits"])[: lab.size].astype(bool)
+    assert dice_delta(lab, ref) <= DICE_TOL
+    assert (lab != ref).mean() <= 1e-4
+    idx = g["big_idx"]
+    np.testing.assert_allclose(seg[0, 0].ravel()[idx], g["big_seg0"], atol=3e-3)
+    np.testing.assert_allclose(seg[0, 1].ravel()[idx], g["big_seg1"], atol=3e-3)
+    np.testing.assert_allclose(mot[0].reshape(4, -1)[:, idx], g["big_mot"], atol=1e-5)
+    np.testing.assert_allclose(seg.astype(np.float64).sum((0, 2, 3, 4)), g["big_seg_sum"], rtol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 48), (1, 3, 8, 16, 32), (3, 3, 24, 32, 32)])
+def test_forward_vs_oracle_other_shapes(model, synthetic_sd, shape):
+    rng = np.random.default_rng(sum(shape))
+    x = rng.uniform(0, 1, shape).astype(np.float32)
+    seg, mot = model(torch.from_numpy(x))
+    rs, rm = r2plus1d_ref.forward(synthetic_sd, x)
+    np.testing.assert_allclose(seg.cpu().numpy(), rs.numpy(), rtol=0, atol=3e-3)
+    np.testing.assert_allclose(mot.cpu().numpy(), rm.numpy(), rtol=0, atol=1e-5)
+
+
+def test_forward_batch_is_per_clip_exact(model):
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy(rng.uniform(0, 1, (4, 3, 32, 112, 112)).astype(np.float32)).cuda()
+    seg, mot = model(x)
+    for i in (0, 3):
+        s1, m1 = model(x[i:i + 1])
+        assert torch.equal(s1[0], seg[i]) and torch.equal(m1[0], mot[i])
+
+
+def test_forward_rejects_bad_shapes(model):
+    with pytest.raises(RuntimeError, match="shape"):
+        model(torch.zeros(1, 3, 12, 112, 112))
+    with pytest.raises(RuntimeError, match="shape"):
+        model(torch.zeros(1, 3, 32, 100, 112))
+
+
+def test_load_state_dict_module_prefix(model, synthetic_sd):
+    import clasfv_amd.weights as W
+    sd2 = W.synthetic_state_dict(99)
+    model.load_state_dict({"module." + k: torch.from_numpy(np.asarray(v)) for k, v in sd2.items()})
+    x = torch.rand(1, 3, 8, 32, 32)
+    s2, _ = model(x)
+    r2, _ = r2plus1d_ref.forward(sd2, x)
+    np.testing.assert_allclose(s2.cpu().numpy(), r2.numpy(), atol=3e-3)
+    model.load_state_dict(synthetic_sd)
+    assert sum(p.numel() for p in model.parameters() if p.requires_grad) == 31_575_731
+
+
+# ---- plumbing kernels ---------------------------------------------------------------------------
+
+def _norm_video(T, seed):
+    import clasfv_amd.synthetic as S
+    return fuse_ref.zeroone_normalizer(S.echo_video(T, seed=seed))
+
+
+@pytest.mark.parametrize("T", [33, 48, 70, 80, 200, 64])
+def test_build_clips_bitexact(T):
+    from clasfv_amd import fuse_utils as FU
+    v = _norm_video(T, T)
+    for interp in (True, False):
+        if not interp and T % 32 and FU.n_clips(T) * 32 > T:
+            continue
+        got = FU.divide_to_consecutive_clips(v, interpolate_last=interp).cpu().numpy()
+        ref = fuse_ref.divide_to_consecutive_clips(v, interpolate_last=interp)
+        np.testing.assert_array_equal(got, ref)
+
+
+@pytest.mark.parametrize("T", [33, 48, 70, 80, 200])
+def test_pipeline_fusion_off_vs_reference_golden(T):
+    from clasfv_amd import fuse_utils as FU
+    g = golden("plumbing.npz")
+    out = FU.segment_a_video_with_fusion(_norm_video(T, T), fake_model, num_clips=1)
+    ref = unpack_labels(g, f"off_T{T}")
+    assert out.dtype == np.int64 and out.shape == ref.shape
+    np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.parametrize("T,f,step", [(70, 5, 1), (200, 5, 1), (80, 3, 2), (48, 10, 1), (40, 5, 3)])
+def test_pipeline_majority_vs_reference_golden(T, f, step):
+    from clasfv_amd import fuse_utils as FU
+    g = golden("plumbing.npz")
+    out = FU.segment_a_video_with_fusion(_norm_video(T, 100 + T), fake_model, step=step, num_clips=f,
+                                         fuse_method="majority")
+    np.testing.assert_array_equal(out, unpack_labels(g, f"on_T{T}_f{f}_s{step}"))
+
+
+@pytest.mark.parametrize("T,f,step", [(70, 5, 1), (80, 3, 2), (48, 10, 1)])
+def test_pipeline_simple_vs_oracle(T, f, step):
+    """SIMPLE fusion: GPU kernel vs the oracle's restatement (parity with LabelFusion unpinned)."""
+    from clasfv_amd import fuse_utils as FU
+
+    def np_model(x):
+        s, m = fake_model(torch.from_numpy(np.ascontiguousarray(x)))
+        return s.numpy(), m.numpy()
+    v = _norm_video(T, 100 + T)
+    out = FU.segment_a_video_with_fusion(v, fake_model, step=step, num_clips=f, fuse_method="simple")
+    ref = fuse_ref.segment_a_video_with_fusion(v, np_model, step=step, num_clips=f, fuse_method="simple")
+    np.testing.assert_array_equal(out, ref)
+
+
+def test_pipeline_quirks():
+    from clasfv_amd import fuse_utils as FU
+    with pytest.raises(IndexError):
+        FU.segment_a_video_with_fusion(_norm_video(32, 32), fake_model, num_clips=1)
+
+
+def test_pipeline_real_model_T48_vs_reference_golden(model):
+    from clasfv_amd import fuse_utils as FU
+    g = golden("pipeline_model_T48.npz")
+    out = FU.segment_a_video_with_fusion(_norm_video(48, 48), model, num_clips=1)
+    ref = np.unpackbits(g["labels"])[: out.size].reshape(out.shape)
+    assert dice_delta(out, ref) <= DICE_TOL
+
+
+def test_normalizer_bitexact_vs_reference_golden():
+    import clasfv_amd.synthetic as S
+    from clasfv_amd.preprocess import zeroone_normalizer
+    g = golden("normalizer.npz")
+    out = zeroone_normalizer(S.echo_video(int(g["T"]), seed=int(g["seed"])))
+    np.testing.assert_array_equal(out[:, ::3, ::5, ::7], g["out_sample"])
+    np.testing.assert_allclose(out.astype(np.float64).sum((1, 2, 3)), g["out_sum"], rtol=1e-12)
+
+
+def test_warp_vs_reference_golden():
+    from clasfv_amd.warp import warp
+    g = golden("warp.npz")
+    for name in ("zero", "plus5px", "minus5px_y", "random", "large"):
+        img = g["img_r"] if name in ("random", "large") else g["img"]
+        out = warp(torch.from_numpy(img).cuda(), torch.from_numpy(g["flow_" + name]).cuda()).cpu().numpy()
+        np.testing.assert_allclose(out, g["out_" + name], atol=2e-5, err_msg=name)
+    box = warp(torch.from_numpy(g["box"]).cuda(), torch.zeros(1, 2, 112, 112).cuda()).cpu().numpy()
+    np.testing.assert_allclose(box, g["box_zero"], atol=2e-5)
+
+
+def test_warp_strided_motion_slice_vs_oracle():
+    from clasfv_amd.warp import warp
+    rng = np.random.default_rng(3)
+    img = torch.from_numpy(rng.uniform(0, 1, (2, 3, 40, 56)).astype(np.float32))
+    motion = torch.from_numpy(np.tanh(rng.normal(0, 0.2, (2, 4, 5, 40, 56))).astype(np.float32))
+    out = warp(img.cuda(), motion.cuda()[:, 2:, 3]).cpu()
+    ref = warp_ref.warp(img, motion[:, 2:, 3])
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=2e-5)

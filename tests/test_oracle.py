@@ -1,0 +1,133 @@
+"""Pin the oracle (CPU restatement) against golden vectors produced by the reference code itself
+(tests/golden/make_golden.py). CPU only."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import fuse_ref, r2plus1d_ref, warp_ref
+from tests.conftest import golden, unpack_labels
+from tests.golden.fake_model import fake_model
+
+
+def _np_model(x):
+    seg, mot = fake_model(torch.from_numpy(np.ascontiguousarray(x)))
+    return seg.numpy(), mot.numpy()
+
+
+def test_param_count_and_keys(synthetic_sd):
+    import clasfv_amd.arch as A
+    g = golden("model_forward.npz")
+    assert int(g["nparams"]) == A.NUM_PARAMS_REFERENCE == A.count_parameters()
+    assert list(g["keys"]) == list(A.state_dict_spec().keys()) == list(synthetic_sd.keys())
+
+
+def test_oracle_forward_small_matches_reference(synthetic_sd):
+    g = golden("model_forward.npz")
+    seg, mot = r2plus1d_ref.forward(synthetic_sd, g["x_small"])
+    np.testing.assert_allclose(seg.numpy(), g["seg_small"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(mot.numpy(), g["mot_small"], rtol=0, atol=1e-6)
+
+
+def test_oracle_forward_full_clip_matches_reference(synthetic_sd):
+    import clasfv_amd.synthetic as S
+    g = golden("model_forward.npz")
+    v = fuse_ref.zeroone_normalizer(S.echo_video(int(g["big_T"]), seed=int(g["big_video_seed"])))
+    s = int(g["big_start"])
+    x = np.ascontiguousarray(v[None, :, s:s + 32])
+    seg, mot = r2plus1d_ref.forward(synthetic_sd, x)
+    seg, mot = seg.numpy(), mot.numpy()
+    lab = (seg[0, 1] > seg[0, 0]).ravel()
+    ref = np.unpackbits(g["big_label_bits"])[: lab.size].astype(bool)
+    assert (lab != ref).sum() <= 2
+    idx = g["big_idx"]
+    np.testing.assert_allclose(seg[0, 0].ravel()[idx], g["big_seg0"], atol=1e-4)
+    np.testing.assert_allclose(seg[0, 1].ravel()[idx], g["big_seg1"], atol=1e-4)
+    np.testing.assert_allclose(mot[0].reshape(4, -1)[:, idx], g["big_mot"], atol=1e-6)
+
+
+@pytest.mark.parametrize("tin,tout", [(200, 192), (192, 200), (33, 32), (32, 33), (70, 64), (64, 70), (80, 64),
+                                      (199, 192), (160, 199), (48, 64)])
+def test_temporal_resample_bitexact_vs_torch(tin, tout):
+    rng = np.random.default_rng(tin * 1000 + tout)
+    x = rng.random((2, tin, 24, 20), dtype=np.float32)
+    ref = F.interpolate(torch.from_numpy(x)[None], size=(tout, 24, 20), mode="trilinear", align_corners=False)[0]
+    np.testing.assert_array_equal(fuse_ref.temporal_resample(x, tout), ref.numpy())
+
+
+def test_plumbing_fusion_off_matches_reference():
+    import clasfv_amd.synthetic as S
+    g = golden("plumbing.npz")
+    for T in (33, 48, 70, 80, 200):
+        v = fuse_ref.zeroone_normalizer(S.echo_video(T, seed=T))
+        out = fuse_ref.segment_a_video_with_fusion(v, _np_model, num_clips=1)
+        ref = unpack_labels(g, f"off_T{T}")
+        assert out.shape == ref.shape and out.dtype == np.int64
+        np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.parametrize("T,f,step", [(70, 5, 1), (200, 5, 1), (80, 3, 2), (48, 10, 1), (40, 5, 3)])
+def test_plumbing_fusion_on_matches_reference(T, f, step):
+    """Vote gathering / frame indexing of the reference with majority voting as fuse_images."""
+    import clasfv_amd.synthetic as S
+    g = golden("plumbing.npz")
+    v = fuse_ref.zeroone_normalizer(S.echo_video(T, seed=100 + T))
+    out = fuse_ref.segment_a_video_with_fusion(v, _np_model, step=step, num_clips=f, fuse_method="majority")
+    np.testing.assert_array_equal(out, unpack_labels(g, f"on_T{T}_f{f}_s{step}"))
+    k = fuse_ref.clamp_num_clips(T, f, step)
+    votes = [sum(1 for idx in range(min(i, k)) if i - idx * step >= 0) for i in range(1, T) if step - 1 < i]
+    ref_votes = g[f"votes_T{T}_f{f}_s{step}"]
+    assert [v_ for v_ in votes if v_ > 1] == list(ref_votes)
+
+
+def test_plumbing_quirks():
+    import clasfv_amd.synthetic as S
+    g = golden("plumbing.npz")
+    assert str(g["err_T32"]) == "IndexError"
+    with pytest.raises(IndexError):
+        fuse_ref.segment_a_video_with_fusion(fuse_ref.zeroone_normalizer(S.echo_video(32, seed=32)), _np_model,
+                                             num_clips=1)
+    clips = fuse_ref.divide_to_consecutive_clips(fuse_ref.zeroone_normalizer(S.echo_video(80, seed=80)), interpolate_last=True)
+    assert tuple(clips.shape) == tuple(g["clips80_shape"])
+    np.testing.assert_allclose(clips.sum((1, 2, 3, 4)), g["clips80_sum"], rtol=1e-6)
+    np.testing.assert_array_equal(clips[:, :, ::7, ::13, ::11], g["clips80_sample"])
+    assert fuse_ref.n_clip_frames(80) == 64 and fuse_ref.n_clip_frames(48) == 64 and fuse_ref.n_clip_frames(47) == 32
+
+
+def test_pipeline_real_model_T48(synthetic_sd):
+    import clasfv_amd.synthetic as S
+    g = golden("pipeline_model_T48.npz")
+    v = fuse_ref.zeroone_normalizer(S.echo_video(48, seed=48))
+    model = r2plus1d_ref.OracleModel(synthetic_sd)
+    out = fuse_ref.segment_a_video_with_fusion(v, model, num_clips=1, to_numpy=lambda t: t.numpy())
+    ref = np.unpackbits(g["labels"])[: out.size].reshape(out.shape)
+    assert (out != ref).sum() <= 4
+
+
+def test_normalizer_matches_reference():
+    import clasfv_amd.synthetic as S
+    g = golden("normalizer.npz")
+    out = fuse_ref.zeroone_normalizer(S.echo_video(int(g["T"]), seed=int(g["seed"])))
+    np.testing.assert_array_equal(out[:, ::3, ::5, ::7], g["out_sample"])
+    np.testing.assert_allclose(out.astype(np.float64).sum((1, 2, 3)), g["out_sum"], rtol=1e-12)
+
+
+def test_warp_oracle_matches_reference():
+    g = golden("warp.npz")
+    for name in ("zero", "plus5px", "minus5px_y", "random", "large"):
+        img = g["img_r"] if name in ("random", "large") else g["img"]
+        out = warp_ref.warp(torch.from_numpy(img), torch.from_numpy(g["flow_" + name])).numpy()
+        np.testing.assert_allclose(out, g["out_" + name], atol=1e-6, err_msg=name)
+    box = warp_ref.warp(torch.from_numpy(g["box"]), torch.zeros(1, 2, 112, 112)).numpy()
+    np.testing.assert_allclose(box, g["box_zero"], atol=1e-6)
+    # zero flow is not the identity (corner-aligned grid, align_corners=False sampling)
+    assert np.abs(box - g["box"]).max() > 0.1
+
+
+def test_simple_vote_properties():
+    rng = np.random.default_rng(0)
+    a = (rng.random((16, 16)) > 0.5).astype(np.uint8)
+    # unanimous votes are returned unchanged; two identical + one different -> the majority
+    np.testing.assert_array_equal(fuse_ref.simple_vote([a, a, a]), a)
+    np.testing.assert_array_equal(fuse_ref.simple_vote([a, a, 1 - a]), a)
+    np.testing.assert_array_equal(fuse_ref.majority_vote([a, 1 - a]), np.zeros_like(a))
