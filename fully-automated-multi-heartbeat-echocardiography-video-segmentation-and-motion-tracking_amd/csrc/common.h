@@ -41,6 +41,8 @@ struct DecParams {
 };
 
 // Launchers (stream-ordered, no synchronisation). Return hipError_t of the launch.
-hipError_t launch_conv(const ConvParams& p, int bn, hipStream_t s);
+hipError_t launch_conv(const ConvParams& p, int bn, int bk, hipStream_t s);
+// N tile (output channels per block) for a padded channel count; force_nt > 0 picks 16*force_nt if it divides.
+int conv_tile_n(int cout_p, int force_nt);
 hipError_t launch_decoder(const DecParams& p, hipStream_t s);
 hipError_t launch_pack_input(const float* x, float* y, int N, int T, int HW, hipStream_t s);

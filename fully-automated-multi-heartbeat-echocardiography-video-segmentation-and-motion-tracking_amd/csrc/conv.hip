@@ -20,17 +20,28 @@
 
 namespace {
 
-template <int MT, int NT, int WM, int WN, bool SMALLC>
-__global__ __launch_bounds__(64 * WM * WN) void conv_igemm_f32(ConvParams p) {
+// XCD-aware tile order: hardware deals blocks round-robin over the 8 XCDs (b % 8 share one L2).
+// Give each XCD a contiguous range of logical tiles (bijective for any count), and walk the N tiles
+// of one M tile consecutively, so the blocks that re-read an im2col A tile (and the 3x3 halo rows of
+// its neighbours) hit the same L2.
+__device__ inline int xcd_swizzle(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+template <int MT, int NT, int WM, int WN, int BK, bool SMALLC>
+__global__ __launch_bounds__(64 * WM * WN) void conv_igemm_f32(ConvParams p, int n_tiles) {
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN, NTH = 64 * WM * WN;
-  constexpr int A4 = BM * 4, B4 = BN * 4;
+  constexpr int KQ = BK / 4;  // float4 columns per tile row
+  constexpr int A4 = BM * KQ, B4 = BN * KQ;
   constexpr int AL = (A4 + NTH - 1) / NTH, BL = (B4 + NTH - 1) / NTH;
-  __shared__ f32x4 As[2][4][BM];
-  __shared__ f32x4 Bs[2][4][BN];
+  __shared__ f32x4 As[2][KQ][BM];
+  __shared__ f32x4 Bs[2][KQ][BN];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int m0 = (tile / n_tiles) * BM, n0 = (tile % n_tiles) * BN;
   const int q = lane >> 4, l16 = lane & 15;
 
   // Per-thread A-load descriptors (fixed over the K loop).
@@ -39,9 +50,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_f32(ConvParams p) {
 #pragma unroll
   for (int i = 0; i < AL; ++i) {
     const int e = tid + i * NTH;
-    const int r = e >> 2;
+    const int r = e / KQ;
     a_r[i] = r;
-    a_q[i] = e & 3;
+    a_q[i] = e % KQ;
     int m = m0 + r;
     a_ok[i] = (e < A4) && (m < p.M);
     if (!a_ok[i]) m = 0;
@@ -61,7 +72,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_f32(ConvParams p) {
 
   auto load_tiles = [&](int k0) {
     int tap_u = 0, c_u = 0;
-    if (!SMALLC) {
+    if (!SMALLC) {  // Cin % BK == 0: the whole BK slice lies in one tap
       tap_u = k0 / p.Cin;
       c_u = k0 - tap_u * p.Cin;
     }
@@ -95,7 +106,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_f32(ConvParams p) {
       const int e = tid + i * NTH;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
       if (e < B4) {
-        const int r = e >> 2, qq = e & 3;
+        const int r = e / KQ, qq = e % KQ;
         v = *reinterpret_cast<const f32x4*>(p.w + (size_t)(n0 + r) * p.Kp + k0 + 4 * qq);
       }
       rb[i] = v;
@@ -108,7 +119,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_f32(ConvParams p) {
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
       const int e = tid + i * NTH;
-      if (e < B4) Bs[buf][e & 3][e >> 2] = rb[i];
+      if (e < B4) Bs[buf][e % KQ][e / KQ] = rb[i];
     }
   };
 
@@ -118,26 +129,29 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_f32(ConvParams p) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.Kp / 16;
+  const int nk = p.Kp / BK;
   load_tiles(0);
   store_tiles(0);
   __syncthreads();
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
-    if (more) load_tiles((kt + 1) * 16);
-    f32x4 a[MT], b[NT];
+    if (more) load_tiles((kt + 1) * BK);
 #pragma unroll
-    for (int i = 0; i < MT; ++i) a[i] = As[cur][q][wm * 16 * MT + i * 16 + l16];
+    for (int s = 0; s < BK / 16; ++s) {
+      f32x4 a[MT], b[NT];
 #pragma unroll
-    for (int j = 0; j < NT; ++j) b[j] = Bs[cur][q][wn * 16 * NT + j * 16 + l16];
+      for (int i = 0; i < MT; ++i) a[i] = As[cur][4 * s + q][wm * 16 * MT + i * 16 + l16];
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
+      for (int j = 0; j < NT; ++j) b[j] = Bs[cur][4 * s + q][wn * 16 * NT + j * 16 + l16];
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+      for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-        for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][kk], b[j][kk], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][kk], b[j][kk], acc[i][j], 0, 0, 0);
+    }
     if (more) store_tiles(cur ^ 1);
     __syncthreads();
     cur ^= 1;
@@ -165,23 +179,46 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_f32(ConvParams p) {
   }
 }
 
-template <int MT, int NT, int WM, int WN>
+template <int MT, int NT, int WM, int WN, int BK, bool SMALLC>
 hipError_t launch_cfg(const ConvParams& p, hipStream_t s) {
   constexpr int BM = 16 * MT * WM, BN = 16 * NT * WN;
-  dim3 grid((p.M + BM - 1) / BM, (p.Cout + BN - 1) / BN);
-  dim3 block(64 * WM * WN);
-  if (p.Cin % 16 == 0)
-    hipLaunchKernelGGL((conv_igemm_f32<MT, NT, WM, WN, false>), grid, block, 0, s, p);
-  else
-    hipLaunchKernelGGL((conv_igemm_f32<MT, NT, WM, WN, true>), grid, block, 0, s, p);
+  const int mt = (p.M + BM - 1) / BM, nt = (p.Cout + BN - 1) / BN;
+  hipLaunchKernelGGL((conv_igemm_f32<MT, NT, WM, WN, BK, SMALLC>), dim3(mt * nt), dim3(64 * WM * WN), 0, s, p, nt);
   return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch_conv(const ConvParams& p, int bn, hipStream_t s) {
-  if (bn == 48) return launch_cfg<2, 3, 4, 1>(p, s);
-  return launch_cfg<2, 4, 4, 1>(p, s);
+int conv_tile_n(int cout_p, int force_nt) {
+  const int n16 = cout_p / 16;
+  if (force_nt > 0 && n16 % force_nt == 0) return 16 * force_nt;
+  for (int nt : {9, 8, 6, 5, 4, 3})
+    if (n16 % nt == 0) return 16 * nt;
+  return 48;
+}
+
+hipError_t launch_conv(const ConvParams& p, int bn, int bk, hipStream_t s) {
+  if (p.Cin % 16 != 0) return launch_cfg<2, 3, 4, 1, 16, true>(p, s);
+  if (bk == 16) {
+    switch (bn) {
+      case 48: return launch_cfg<2, 3, 4, 1, 16, false>(p, s);
+      case 64: return launch_cfg<2, 4, 4, 1, 16, false>(p, s);
+      case 80: return launch_cfg<2, 5, 4, 1, 16, false>(p, s);
+      case 96: return launch_cfg<2, 6, 4, 1, 16, false>(p, s);
+      case 128: return launch_cfg<2, 8, 4, 1, 16, false>(p, s);
+      case 144: return launch_cfg<2, 9, 4, 1, 16, false>(p, s);
+    }
+  } else {
+    switch (bn) {
+      case 48: return launch_cfg<2, 3, 4, 1, 32, false>(p, s);
+      case 64: return launch_cfg<2, 4, 4, 1, 32, false>(p, s);
+      case 80: return launch_cfg<2, 5, 4, 1, 32, false>(p, s);
+      case 96: return launch_cfg<2, 6, 4, 1, 32, false>(p, s);
+      case 128: return launch_cfg<2, 8, 4, 1, 32, false>(p, s);
+      case 144: return launch_cfg<2, 9, 4, 1, 32, false>(p, s);
+    }
+  }
+  return hipErrorInvalidValue;
 }
 
 // (N,3,T,H,W) fp32 -> channels-last (N,T,H,W,4) with channel 3 = 0.

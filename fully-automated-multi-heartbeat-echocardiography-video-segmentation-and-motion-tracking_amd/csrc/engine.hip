@@ -7,6 +7,7 @@
 // (45->48, 230->240, 460->480, 921->960) and uploads everything to HBM once.
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -62,7 +63,7 @@ struct Conv {
   std::string w, bn;  // parameter name prefixes (".weight" / BN module)
   int cin, cout, cin_p, cout_p;
   int kt, kh, kw, st, sh, sw, pt, ph, pw;
-  int K, Kp, bn_tile, cout_alloc;
+  int K, Kp, bn_tile, bk, cout_alloc;
   float* dw = nullptr;
   float* db = nullptr;
 };
@@ -80,7 +81,17 @@ Conv make_conv(Role role, const std::string& w, const std::string& bn, int cin, 
   c.kt = kt, c.kh = kh, c.kw = kw, c.st = st, c.sh = sh, c.sw = sw, c.pt = pt, c.ph = ph, c.pw = pw;
   c.K = kt * kh * kw * c.cin_p;
   c.Kp = round_up(c.K, 16);
-  c.bn_tile = (c.cout_p % 64 == 0) ? 64 : 48;
+  // Tile choice (tunable from the environment for A/B runs: CLASFV_CONV_NT, CLASFV_CONV_BK).
+  const char* env_nt = getenv("CLASFV_CONV_NT");
+  const char* env_bk = getenv("CLASFV_CONV_BK");
+  const int max_bk = env_bk ? atoi(env_bk) : 16;  // BK=32 measured slower (LDS -> 2-3 waves/SIMD)
+  if (c.cin_p % 16 != 0) {
+    c.bn_tile = 48;  // stem: 3 (padded 4) input channels, per-float4 tap decode
+    c.bk = 16;
+  } else {
+    c.bn_tile = conv_tile_n(c.cout_p, env_nt ? atoi(env_nt) : 0);
+    c.bk = (c.cin_p % 32 == 0 && max_bk >= 32) ? 32 : 16;
+  }
   c.cout_alloc = round_up(c.cout_p, c.bn_tile);
   return c;
 }
@@ -231,7 +242,7 @@ int run_conv(const Conv& c, const float* x, const Shape5& in, float* y, Shape5& 
   p.K = c.K, p.Kp = c.Kp;
   p.M = out.n * out.t * out.h * out.w;
   p.relu = relu ? 1 : 0;
-  HIP_TRY(launch_conv(p, c.bn_tile, s));
+  HIP_TRY(launch_conv(p, c.bn_tile, c.bk, s));
   return CLASFV_OK;
 }
 
