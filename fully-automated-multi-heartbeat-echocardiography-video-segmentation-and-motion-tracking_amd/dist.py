@@ -53,29 +53,37 @@ def all_gather_clips(local, n_total, rank, world, group=None):
     return torch.cat(parts)
 
 
+def run_clip_shard(n_total, rank, world, compute, empty):
+    """Run ``compute(lo, hi) -> (hi-lo, ...)`` on this rank's block of the global clip list and
+    all-gather every block: returns the (n_total, ...) result in global clip order on every rank.
+    ``empty`` is a zero-row tensor of the right trailing shape/dtype/device for an idle rank."""
+    lo, hi = shard_bounds(n_total, rank, world)
+    local = compute(lo, hi) if hi > lo else empty
+    return all_gather_clips(local.contiguous(), n_total, rank, world)
+
+
 def segment_videos_sharded(videos_dev, model, num_clips=5, step=1, fuse_method="simple", interpolate_last=True,
                            rank=0, world=1, batch_size=None, clip_fn=None):
     """Fuse a batch of device videos (each (3,T,H,W)) with clips sharded over ranks.
 
     Returns {video index: fused (T',H,W) uint8 device tensor} for the videos this rank owns
-    (v % world == rank). ``clip_fn(clips) -> logits`` overrides the model call (tests)."""
+    (v % world == rank). ``clip_fn(clips) -> logits`` overrides the model call."""
     plans, n_total = global_clip_plan([v.shape[1] for v in videos_dev], num_clips, step, interpolate_last)
-    lo, hi = shard_bounds(n_total, rank, world)
-    # build this rank's clips: per video, the overlap of its clip range with [lo, hi)
-    mine = []
-    for vi, p in enumerate(plans):
-        a, b = max(lo, p["offset"]), min(hi, p["offset"] + p["n"])
-        if a < b:
-            tab = p["table"][a - p["offset"]: b - p["offset"]]
-            mine.append(FU.build_clips(videos_dev[vi], tab, interpolate_last))
     h, w = videos_dev[0].shape[-2:]
     dev = videos_dev[0].device
-    if mine:
+
+    def compute(lo, hi):
+        mine = []
+        for vi, p in enumerate(plans):  # overlap of each video's clip range with [lo, hi)
+            a, b = max(lo, p["offset"]), min(hi, p["offset"] + p["n"])
+            if a < b:
+                mine.append(FU.build_clips(videos_dev[vi], p["table"][a - p["offset"]: b - p["offset"]],
+                                           interpolate_last))
         clips = torch.cat(mine) if len(mine) > 1 else mine[0]
-        logits = clip_fn(clips) if clip_fn else FU.run_model(model, clips, batch_size)
-    else:
-        logits = torch.empty((0, 2, FU.CLIP, h, w), device=dev, dtype=torch.float32)
-    logits = all_gather_clips(logits.contiguous(), n_total, rank, world)
+        return clip_fn(clips) if clip_fn else FU.run_model(model, clips, batch_size)
+
+    empty = torch.empty((0, 2, FU.CLIP, h, w), device=dev, dtype=torch.float32)
+    logits = run_clip_shard(n_total, rank, world, compute, empty)
     out = {}
     for vi, p in enumerate(plans):
         if vi % world != rank:

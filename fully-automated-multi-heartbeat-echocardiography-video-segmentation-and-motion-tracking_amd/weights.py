@@ -76,5 +76,5 @@ def save_checkpoint(path, state_dict, module_prefix=True):
     import torch
     sd = OrderedDict()
     for k, v in state_dict.items():
-        sd[("module." if module_prefix else "") + k] = torch.from_numpy(np.ascontiguousarray(v))
+        sd[("module." if module_prefix else "") + k] = torch.from_numpy(np.array(v, copy=True))
     torch.save({"model": sd}, path)

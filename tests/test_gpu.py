@@ -195,3 +195,21 @@ def test_warp_strided_motion_slice_vs_oracle():
     out = warp(img.cuda(), motion.cuda()[:, 2:, 3]).cpu()
     ref = warp_ref.warp(img, motion[:, 2:, 3])
     np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=2e-5)
+
+
+def test_cli_end_to_end(tmp_path):
+    """motion_segment.py drop-in: pickles with the reference names, EF text, int64 masks."""
+    import pickle
+    import subprocess
+    import sys
+    import clasfv_amd.synthetic as S
+    vid = tmp_path / "echo_case.npy"
+    np.save(vid, S.echo_video_uint8(100, seed=4))
+    r = subprocess.run([sys.executable, "motion_segment.py", "-p", str(vid), "--synthetic-weights", "1234", "-f", "2",
+                        "-c", "binary,binary_video", "-o", str(tmp_path), "-v"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "R2+1D MotionNet has 31575731 parameters." in r.stdout
+    assert "systoles" in r.stdout
+    whole = pickle.load(open(tmp_path / "echo_case_whole_video_segmentation.pkl", "rb"))
+    assert whole.shape == (100, 112, 112) and whole.dtype == np.int64

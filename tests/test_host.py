@@ -1,0 +1,178 @@
+"""CPU tests: C-ABI library load + exports, host-side logic (clip plans, weights, checkpoints, EF),
+and the multi-rank clip sharding over gloo (world_size 2 and 3)."""
+import ctypes
+import os
+import re
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import REPO, golden
+
+HEADER = os.path.join(REPO, "include", "clasfv.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int64_t|int|void)\s+\*?(clasfv_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_builds_and_exports_every_header_symbol():
+    from clasfv_amd import _lib
+    from clasfv_amd.build import build
+    path = build()
+    assert os.path.exists(path)
+    lib = ctypes.CDLL(path)
+    funcs = header_functions()
+    assert len(funcs) >= 14
+    for f in funcs:
+        assert hasattr(lib, f), f"{f} declared in include/clasfv.h but not exported"
+    assert set(funcs) == set(_lib.SIGNATURES), "ctypes signatures out of sync with include/clasfv.h"
+
+
+def test_library_reports_errors_without_gpu():
+    from clasfv_amd import _lib
+    lib = _lib.load()
+    assert lib.clasfv_version() == 1
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = ctypes.c_void_p()
+    rc = lib.clasfv_create(0, ctypes.byref(h))
+    assert rc != 0 and lib.clasfv_last_error()
+    assert lib.clasfv_forward(None, None, 1, 32, 112, 112, None, None, None) == -1  # CLASFV_EINVAL
+
+
+def test_product_path_has_no_oracle_or_cpu_fallback():
+    pkg = os.path.join(REPO, "fully-automated-multi-heartbeat-echocardiography-video-segmentation-and-motion-tracking_amd")
+    for f in os.listdir(pkg):
+        if f.endswith(".py"):
+            src = open(os.path.join(pkg, f)).read()
+            assert "oracle" not in re.sub(r'""".*?"""', "", src, flags=re.S).replace("# ", ""), f
+
+
+def test_arch_spec_matches_reference_counts():
+    import clasfv_amd.arch as A
+    spec = A.state_dict_spec()
+    assert len(spec) == 242
+    assert A.count_parameters(spec) == A.NUM_PARAMS_REFERENCE
+    mids = [c.cout for r, c in A.backbone_convs() if r == "sp1"]
+    assert mids == [144, 144, 230, 288, 460, 576, 921, 1152]
+    assert sum(1 for k in spec if k.endswith("num_batches_tracked")) == 39
+
+
+def test_synthetic_weights_deterministic():
+    import clasfv_amd.weights as W
+    a = W.synthetic_state_dict(7)
+    b = W.synthetic_state_dict(7)
+    c = W.synthetic_state_dict(8)
+    assert all(np.array_equal(a[k], b[k]) for k in a)
+    assert not np.array_equal(a["comb_1_layer.weight"], c["comb_1_layer.weight"])
+    assert all(v.dtype == np.float32 for k, v in a.items() if not k.endswith("num_batches_tracked"))
+
+
+def test_checkpoint_roundtrip_with_module_prefix(tmp_path):
+    import clasfv_amd.weights as W
+    sd = W.synthetic_state_dict(3)
+    p = str(tmp_path / "ckpt.pth")
+    W.save_checkpoint(p, sd, module_prefix=True)
+    raw = torch.load(p, weights_only=True)
+    assert next(iter(raw["model"])).startswith("module.")
+    back = W.load_checkpoint(p)
+    assert list(back) == list(sd) and all(np.array_equal(back[k], sd[k]) for k in sd)
+
+
+@pytest.mark.parametrize("T", [33, 40, 47, 48, 64, 70, 80, 100, 199, 200, 256])
+@pytest.mark.parametrize("f,step", [(1, 1), (5, 1), (3, 2), (10, 1), (5, 3)])
+def test_clip_plan_matches_oracle(T, f, step):
+    from clasfv_amd import fuse_utils as FU
+    from oracle import fuse_ref
+    k = FU.clamp_num_clips(T, f, step)
+    assert k == fuse_ref.clamp_num_clips(T, f, step)
+    if k == 0:
+        return
+    table, clip0 = FU.clip_table(T, k, step)
+    for j in range(k):
+        n_ref = len(range(0, fuse_ref.n_clip_frames(T - j * step), 32))
+        nxt = clip0[j + 1] if j + 1 < k else len(table)
+        assert nxt - clip0[j] == n_ref
+        assert all(s == j * step for s, _ in table[clip0[j]:nxt])
+
+
+def test_ef_matches_reference_golden():
+    from clasfv_amd.echo import compute_ef_using_putative_clips, get2dPucks
+    g = golden("ef.npz")
+    for name in g["names"]:
+        shp = tuple(g[name + "_shape"])
+        m = np.unpackbits(g[name + "_bits"])[: int(np.prod(shp))].reshape(shp).astype(np.int64)
+        efs, pairs = compute_ef_using_putative_clips(m, name, return_edes=True)
+        assert np.array(pairs, np.int64).reshape(-1, 2).tolist() == g[name + "_pairs"].tolist(), name
+        np.testing.assert_allclose(np.array(efs, np.float64), g[name + "_efs"], rtol=0, atol=1e-9, equal_nan=True)
+    fr = np.unpackbits(g["pucks_frames"]).reshape(-1, 112, 112)
+    for i, f in enumerate(fr):
+        L, R = get2dPucks(f.astype(int), (1.0, 1.0))
+        assert L == g["pucks_L"][i]
+        np.testing.assert_array_equal(R, g["pucks_R"][i])
+    # SURVEY §8c known answer: four ED-ES pairs of the pulsing ellipse, EF 68.808074 each
+    np.testing.assert_allclose(g["ellipse200_efs"], 68.808074, atol=1e-6)
+
+
+def test_synthetic_video_and_lv_masks():
+    import clasfv_amd.synthetic as S
+    v = S.echo_video_uint8(60, seed=0)
+    assert v.shape == (60, 112, 112, 3) and v.dtype == np.uint8
+    assert np.array_equal(v[..., 0], v[..., 2])
+    m = S.ellipse_masks(60)
+    area = m.sum((1, 2))
+    assert area.argmax() in (0, 50) and abs(int(area.argmin()) - 25) <= 1
+
+
+def test_shard_bounds_partition():
+    from clasfv_amd.dist import shard_bounds
+    for n in (0, 1, 7, 30, 31, 384, 1920):
+        for world in (1, 2, 3, 4, 8):
+            spans = [shard_bounds(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gloo_worker(rank, world, port, n_total, q):
+    import torch.distributed as dist
+    from clasfv_amd.dist import run_clip_shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def compute(lo, hi):  # stand-in per-clip "logits": a function of the global clip index only
+            idx = torch.arange(lo, hi, dtype=torch.float32)
+            return idx[:, None, None] * 10 + torch.arange(6, dtype=torch.float32).view(1, 2, 3)
+        out = run_clip_shard(n_total, rank, world, compute, torch.empty((0, 2, 3)))
+        q.put((rank, out.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total", [(2, 30), (2, 1), (3, 31), (2, 0)])
+def test_clip_shard_all_gather_gloo(world, n_total):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    ref = np.arange(n_total, dtype=np.float32)[:, None, None] * 10 + np.arange(6, dtype=np.float32).reshape(1, 2, 3)
+    for r in range(world):
+        np.testing.assert_array_equal(res[r], ref)
