@@ -42,7 +42,6 @@ def parse():
     ap.add_argument("--batch-size", type=int, default=32, help="clips per forward call")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--cpu-sample-clips", type=int, default=4)
-    ap.add_argument("--no-parity", action="store_true")
     return ap.parse_args()
 
 
@@ -120,9 +119,9 @@ def main():
     # on-line sanity figure: LV fraction of the last step's masks.
     lv_frac = float(np.mean([o.float().mean().item() for o in out.values()])) if out else 0.0
 
-    cpu = None
+    cpu, dice = None, None
     if rank == 0 and world == 1 and args.cpu_baseline:
-        cpu = cpu_baseline(args, S)
+        cpu, dice = cpu_baseline(args, S, model)
 
     if rank == 0:
         line = {
@@ -144,10 +143,14 @@ def main():
                        "step": args.step, "clips_per_step": clips_per_step, "batch_size": args.batch_size,
                        "parallelism": f"clip-shard x{world}, all-gather of per-clip logits"},
             "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                         "unit": "TFLOP/s", "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
+                         "traffic": (profiled_traffic() or {}).get("bytes_per_forward"),
+                         "traffic_note": "HBM bytes per forward launch sequence (30 clips), rocprofv3 PMC "
+                                         "FETCH_SIZE x2 + WRITE_SIZE from " + str((profiled_traffic() or {}).get("source")),
                          "kernel": "model forward (clasfv_forward: 41 conv_igemm + decoder launches)",
                          "gflop_per_clip": GFLOP_PER_CLIP, "forward_ms_per_clip": round(fwd_ms / max(fwd_clips, 1), 4)},
             "cpu_baseline": cpu,
+            "dice_delta_vs_cpu": dice,
             "lv_fraction": round(lv_frac, 4),
         }
         print(json.dumps(line), flush=True)
@@ -155,10 +158,28 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, S):
+def profiled_traffic():
+    """HBM bytes per forward launch sequence from the committed rocprofv3 PMC summary
+    (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or None."""
+    import glob
+    import re
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_kernel_stats.txt")))
+    if not files:
+        return None
+    txt = open(files[-1]).read()
+    f = re.search(r"FETCH_SIZE last forward: [\d.]+ MiB raw, x2 corrected = ([\d.]+) MiB", txt)
+    w = re.search(r"WRITE_SIZE last forward: [\d.]+ MiB raw, x1 corrected = ([\d.]+) MiB", txt)
+    if not (f and w):
+        return None
+    return {"bytes_per_forward": int((float(f.group(1)) + float(w.group(1))) * 2**20),
+            "clips_per_forward": 30, "source": os.path.basename(files[-1])}
+
+
+def cpu_baseline(args, S, gpu_model):
     """Reference-style CPU path (oracle = op-for-op restatement of the reference, torch CPU):
     per-clip batch-1 forwards as src/fuse_utils.py:53-61 does, on a bounded sample of clips, plus the
-    CPU plumbing of one whole video with the clip forwards replaced by cached logits."""
+    CPU plumbing of one whole video with the clip forwards replaced by cached logits.
+    Also returns the Dice delta (1 - Dice of the LV masks) of the GPU forward vs these CPU clips."""
     from oracle import fuse_ref, r2plus1d_ref
     import clasfv_amd.weights as W
     threads = min(os.cpu_count() or 1, 16)
@@ -171,11 +192,18 @@ def cpu_baseline(args, S):
     t0 = time.perf_counter()
     n = 0
     cached = None
+    cpu_masks = []
     for i in range(args.cpu_sample_clips):
         seg, _ = model(clips[i % len(clips)][None])
         cached = (seg.numpy(), None)
+        cpu_masks.append(seg[0, 1].numpy() > seg[0, 0].numpy())
         n += 1
     t_clip = (time.perf_counter() - t0) / n
+    from clasfv_amd.echo import categorical_dice
+    gseg, _ = gpu_model(torch.from_numpy(np.stack([clips[i % len(clips)] for i in range(n)])))
+    gseg = gseg.cpu().numpy()
+    gpu_masks = gseg[:, 1] > gseg[:, 0]
+    dice = float(1.0 - categorical_dice(gpu_masks, np.stack(cpu_masks), 1))
     t1 = time.perf_counter()
     k = fuse_ref.clamp_num_clips(args.frames, args.fuse, args.step)
     out = fuse_ref.segment_a_video_with_fusion(v, lambda c: cached, step=args.step, num_clips=args.fuse,
@@ -187,7 +215,7 @@ def cpu_baseline(args, S):
             "sample": f"{n} batch-1 clip forwards of the torch-CPU oracle ({t_clip:.2f} s/clip) + CPU plumbing "
                       f"and SIMPLE fusion of one {args.frames}-frame video ({t_plumb:.2f} s), extrapolated to "
                       f"the {n_total} clips of one step",
-            "out_shape": list(out.shape)}
+            "out_shape": list(out.shape)}, round(dice, 7)
 
 
 if __name__ == "__main__":
