@@ -19,6 +19,9 @@ struct ConvParams {
   int To, Ho, Wo, Cout;
   int KT, KH, KW, st, sh, sw, pt, ph, pw;
   int K, Kp, M, relu;
+  const float* zero;  // >= 16 zero bytes (source of padding taps for the LDS-DMA path)
+  const float* x2;    // optional second input of a 1x1x1 conv (same voxels), K columns after x's
+  int Cin2;
 };
 
 // Decoder tap: low-resolution projection P_i = (s1 * W_i) . f_i, channels-last with 64 channels.
@@ -41,8 +44,8 @@ struct DecParams {
 };
 
 // Launchers (stream-ordered, no synchronisation). Return hipError_t of the launch.
-hipError_t launch_conv(const ConvParams& p, int bn, int bk, hipStream_t s);
-// N tile (output channels per block) for a padded channel count; force_nt > 0 picks 16*force_nt if it divides.
-int conv_tile_n(int cout_p, int force_nt);
+hipError_t launch_conv(const ConvParams& p, int mt, int bn, hipStream_t s);
+// Block tile (BM = 64*mt rows, bn output channels) for an M x cout_p conv.
+void conv_pick_tile(int M, int cout_p, int force_nt, int* mt, int* bn);
 hipError_t launch_decoder(const DecParams& p, hipStream_t s);
 hipError_t launch_pack_input(const float* x, float* y, int N, int T, int HW, hipStream_t s);

@@ -23,8 +23,10 @@ constexpr int PIX = 68;  // floats per staged pixel: 64 channels + 4 pad (fewer 
 constexpr int TILE_H = 8, TILE_W = 16;
 __constant__ const int kMaxRows[4] = {6, 4, 3, 3};
 __constant__ const int kMaxCols[4] = {10, 6, 4, 3};
-constexpr int kPixOff[5] = {0, 2 * 6 * 10, 2 * 6 * 10 + 2 * 4 * 6, 2 * 6 * 10 + 2 * 4 * 6 + 2 * 3 * 4,
-                            2 * 6 * 10 + 2 * 4 * 6 + 2 * 3 * 4 + 2 * 3 * 3};
+// tap 0 (stem + layer1) keeps the clip's frame rate: its temporal scale is exactly 1, one frame.
+constexpr int kFrames[4] = {1, 2, 2, 2};
+constexpr int kPixOff[5] = {0, 1 * 6 * 10, 1 * 6 * 10 + 2 * 4 * 6, 1 * 6 * 10 + 2 * 4 * 6 + 2 * 3 * 4,
+                            1 * 6 * 10 + 2 * 4 * 6 + 2 * 3 * 4 + 2 * 3 * 3};
 constexpr int STAGE_FLOATS = kPixOff[4] * PIX;
 
 struct Win {
@@ -40,10 +42,9 @@ __device__ inline void src_index(float s, int dst, int in, int& i0, int& i1, flo
   l0 = 1.f - l1;
 }
 
-__global__ __launch_bounds__(256) void decoder_kernel(DecParams p) {
+__global__ __launch_bounds__(256, 4) void decoder_kernel(DecParams p) {
   extern __shared__ __align__(16) float smem[];
-  float* stage = smem;                                      // STAGE_FLOATS
-  f32x4* w2s = reinterpret_cast<f32x4*>(smem + STAGE_FLOATS);  // [16 k4][64 n] float4
+  float* stage = smem;  // STAGE_FLOATS
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int q = lane >> 4, l16 = lane & 15;
@@ -51,11 +52,6 @@ __global__ __launch_bounds__(256) void decoder_kernel(DecParams p) {
   const int h0 = (blockIdx.x / tiles_w) * TILE_H, w0 = (blockIdx.x % tiles_w) * TILE_W;
   const int t = blockIdx.y, n = blockIdx.z;
 
-  // W2 (64x64, [n][k]) -> LDS k4-major: w2s[kq*64 + n] = W2[n][4kq .. 4kq+3]
-  for (int e = tid; e < 16 * 64; e += 256) {
-    const int nn = e & 63, kq = e >> 6;
-    w2s[kq * 64 + nn] = *reinterpret_cast<const f32x4*>(p.w2 + nn * 64 + kq * 4);
-  }
 
   // Source windows of the four taps.
   Win win[4];
@@ -70,7 +66,7 @@ __global__ __launch_bounds__(256) void decoder_kernel(DecParams p) {
     w.t1 = b;
     w.lt0 = la;
     w.lt1 = lb;
-    w.nf = (lb > 0.f && b != a) ? 2 : 1;
+    w.nf = (lb > 0.f && b != a) ? min(2, kFrames[i]) : 1;
     const int r0 = min((int)floorf(tp.sh * (float)h0), tp.H - 1);
     const int r1 = min((int)floorf(tp.sh * (float)(h0 + TILE_H - 1)) + 1, tp.H - 1);
     const int c0 = min((int)floorf(tp.sw * (float)w0), tp.W - 1);
@@ -98,120 +94,91 @@ __global__ __launch_bounds__(256) void decoder_kernel(DecParams p) {
   }
   __syncthreads();
 
-  // ---- 2. interpolation: lane = (voxel column l16, channel group q); h1[mt][4c + j] = ch 16c+4q+j
-  f32x4 h1[2][4];
+  // ---- per voxel row (mt): 2. interpolate, 3. comb_2 on MFMA, 4. heads on MFMA, 5. store.
+  // lane = (voxel column l16, channel group q): h1[c][j] holds channel 16c + 4q + j.
+  const size_t HW = (size_t)p.H * p.W;
+  const size_t TH = (size_t)p.T * HW;
+  f32x4 wh[4];
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b1 + 16 * c + 4 * q);
-    h1[0][c] = bb;
-    h1[1][c] = bb;
+  for (int nt = 0; nt < 4; ++nt) {
+    wh[nt] = *reinterpret_cast<const f32x4*>(p.wh + (l16 & 7) * 64 + 16 * nt + 4 * q);
+    if (l16 >= 8) wh[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+#pragma unroll 1
+  for (int mt = 0; mt < 2; ++mt) {
+    const int hr = h0 + 2 * wid + mt;
+    f32x4 h1[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const DecTap& tp = p.tap[i];
-    const Win& w = win[i];
-    const float* src = stage + kPixOff[i] * PIX;
-    const int wc = w0 + l16;
-    int x0, x1;
-    float lx0, lx1;
-    src_index(tp.sw, wc, tp.W, x0, x1, lx0, lx1);
-    x0 -= w.c0;
-    x1 -= w.c0;
+    for (int c = 0; c < 4; ++c) h1[c] = *reinterpret_cast<const f32x4*>(p.b1 + 16 * c + 4 * q);
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const int hr = h0 + 2 * wid + mt;
-      int y0, y1;
-      float ly0, ly1;
+    for (int i = 0; i < 4; ++i) {
+      const DecTap& tp = p.tap[i];
+      const Win& w = win[i];
+      int x0, x1, y0, y1;
+      float lx0, lx1, ly0, ly1;
+      src_index(tp.sw, w0 + l16, tp.W, x0, x1, lx0, lx1);
       src_index(tp.sh, hr, tp.H, y0, y1, ly0, ly1);
+      x0 -= w.c0;
+      x1 -= w.c0;
       y0 -= w.r0;
       y1 -= w.r0;
+      const float* src = stage + kPixOff[i] * PIX + 4 * q;
       for (int f = 0; f < w.nf; ++f) {
         const float wt = f ? w.lt1 : w.lt0;
         const float* fb = src + f * w.nr * w.nc * PIX;
-        const float* p00 = fb + (y0 * w.nc + x0) * PIX + 4 * q;
-        const float* p01 = fb + (y0 * w.nc + x1) * PIX + 4 * q;
-        const float* p10 = fb + (y1 * w.nc + x0) * PIX + 4 * q;
-        const float* p11 = fb + (y1 * w.nc + x1) * PIX + 4 * q;
+        const float* p00 = fb + (y0 * w.nc + x0) * PIX;
+        const float* p01 = fb + (y0 * w.nc + x1) * PIX;
+        const float* p10 = fb + (y1 * w.nc + x0) * PIX;
+        const float* p11 = fb + (y1 * w.nc + x1) * PIX;
+        const float a0 = wt * ly0, a1 = wt * ly1;
+        const float w00 = a0 * lx0, w01 = a0 * lx1, w10 = a1 * lx0, w11 = a1 * lx1;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const f32x4 v00 = *reinterpret_cast<const f32x4*>(p00 + 16 * c);
-          const f32x4 v01 = *reinterpret_cast<const f32x4*>(p01 + 16 * c);
-          const f32x4 v10 = *reinterpret_cast<const f32x4*>(p10 + 16 * c);
-          const f32x4 v11 = *reinterpret_cast<const f32x4*>(p11 + 16 * c);
-          const f32x4 top = v00 * lx0 + v01 * lx1;
-          const f32x4 bot = v10 * lx0 + v11 * lx1;
-          h1[mt][c] += (top * ly0 + bot * ly1) * wt;
+          h1[c] += *reinterpret_cast<const f32x4*>(p00 + 16 * c) * w00;
+          h1[c] += *reinterpret_cast<const f32x4*>(p01 + 16 * c) * w01;
+          h1[c] += *reinterpret_cast<const f32x4*>(p10 + 16 * c) * w10;
+          h1[c] += *reinterpret_cast<const f32x4*>(p11 + 16 * c) * w11;
         }
       }
     }
-  }
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) h1[mt][c][j] = fmaxf(h1[mt][c][j], 0.f);
+      for (int j = 0; j < 4; ++j) h1[c][j] = fmaxf(h1[c][j], 0.f);
 
-  // ---- 3. h2^T[n][v] = sum_k W2[n][k] h1[v][k]; MFMA j of lane group q covers k = 16c + 4q + j
-  f32x4 acc[2][4];
+    // 3. h2^T[n][v] = sum_k W2[n][k] h1[v][k]; MFMA j of lane group q covers k = 16c + 4q + j
+    f32x4 acc[4];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+    for (int nt = 0; nt < 4; ++nt) {
+      acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 wa[4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int c = 0; c < 4; ++c)
+        wa[c] = *reinterpret_cast<const f32x4*>(p.w2 + (nt * 16 + l16) * 64 + 16 * c + 4 * q);
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    f32x4 wa[4];
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) wa[c] = w2s[(c * 4 + q) * 64 + nt * 16 + l16];
+        for (int j = 0; j < 4; ++j)
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[c][j], h1[c][j], acc[nt], 0, 0, 0);
+      // acc[nt][r] = h2^T[ch = 16nt + 4q + r][voxel l16]
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[c][j], h1[mt][c][j], acc[mt][nt], 0, 0, 0);
-  }
-  // acc[mt][nt][r] = h2^T[ch = 16nt + 4q + r][voxel l16]
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[mt][nt][r] = fmaxf(acc[mt][nt][r] + bb[r], 0.f);
-  }
-
-  // ---- 4. heads^T[co][v] = sum_k Wh[co][k] h2^T[k][v]; lane's B operand for (nt, r) is k = 16nt+4q+r
-  f32x4 wh[4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) wh[nt] = *reinterpret_cast<const f32x4*>(p.wh + (l16 & 7) * 64 + 16 * nt + 4 * q);
-  if (l16 >= 8) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) wh[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  f32x4 out[2];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    out[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < 4; ++r) acc[nt][r] = fmaxf(acc[nt][r] + bb[r], 0.f);
+    }
+    // 4. heads^T[co][v] = sum_k Wh[co][k] h2^T[k][v]; the accumulator layout is the B operand
+    f32x4 out = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        out[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[mt][nt][r], out[mt], 0, 0, 0);
-  }
-
-  // ---- 5. out[mt][r] = head (4q + r) at voxel (h0 + 2*wid + mt, w0 + l16)
-  const size_t HW = (size_t)p.H * p.W;
-  const size_t TH = (size_t)p.T * HW;
-  if (q < 2) {
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const size_t pix = (size_t)t * HW + (size_t)(h0 + 2 * wid + mt) * p.W + (w0 + l16);
+      for (int r = 0; r < 4; ++r) out = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[nt][r], out, 0, 0, 0);
+    // 5. out[r] = head (4q + r) at voxel (hr, w0 + l16)
+    if (q < 2) {
+      const size_t pix = (size_t)t * HW + (size_t)hr * p.W + (w0 + l16);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = 4 * q + r;
         if (co >= 6) continue;
-        const float v = out[mt][r] + p.bh[co];
+        const float v = out[r] + p.bh[co];
         if (co < 2)
           p.seg[((size_t)n * 2 + co) * TH + pix] = v;
         else
@@ -224,8 +191,9 @@ __global__ __launch_bounds__(256) void decoder_kernel(DecParams p) {
 }  // namespace
 
 hipError_t launch_decoder(const DecParams& p, hipStream_t s) {
+  if (p.tap[0].T != p.T) return hipErrorInvalidValue;  // tap 0 is staged as a single frame
   dim3 grid((p.H / TILE_H) * (p.W / TILE_W), p.T, p.N);
-  const size_t lds = (size_t)STAGE_FLOATS * 4 + 16 * 64 * 16;
+  const size_t lds = (size_t)STAGE_FLOATS * 4;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)decoder_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

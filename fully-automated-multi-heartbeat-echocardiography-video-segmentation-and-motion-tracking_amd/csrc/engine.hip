@@ -63,7 +63,8 @@ struct Conv {
   std::string w, bn;  // parameter name prefixes (".weight" / BN module)
   int cin, cout, cin_p, cout_p;
   int kt, kh, kw, st, sh, sw, pt, ph, pw;
-  int K, Kp, bn_tile, bk, cout_alloc;
+  int K, Kp, cout_alloc;
+  int cin2 = 0;  // second input of a dual 1x1x1 conv (decoder P01 = W0 f_stem + W1 f_layer1)
   float* dw = nullptr;
   float* db = nullptr;
 };
@@ -81,18 +82,7 @@ Conv make_conv(Role role, const std::string& w, const std::string& bn, int cin, 
   c.kt = kt, c.kh = kh, c.kw = kw, c.st = st, c.sh = sh, c.sw = sw, c.pt = pt, c.ph = ph, c.pw = pw;
   c.K = kt * kh * kw * c.cin_p;
   c.Kp = round_up(c.K, 16);
-  // Tile choice (tunable from the environment for A/B runs: CLASFV_CONV_NT, CLASFV_CONV_BK).
-  const char* env_nt = getenv("CLASFV_CONV_NT");
-  const char* env_bk = getenv("CLASFV_CONV_BK");
-  const int max_bk = env_bk ? atoi(env_bk) : 16;  // BK=32 measured slower (LDS -> 2-3 waves/SIMD)
-  if (c.cin_p % 16 != 0) {
-    c.bn_tile = 48;  // stem: 3 (padded 4) input channels, per-float4 tap decode
-    c.bk = 16;
-  } else {
-    c.bn_tile = conv_tile_n(c.cout_p, env_nt ? atoi(env_nt) : 0);
-    c.bk = (c.cin_p % 32 == 0 && max_bk >= 32) ? 32 : 16;
-  }
-  c.cout_alloc = round_up(c.cout_p, c.bn_tile);
+  c.cout_alloc = c.cout_p;  // every tile width used divides cout_p
   return c;
 }
 
@@ -112,6 +102,7 @@ struct clasfv_engine {
   char* arena = nullptr;
   size_t arena_bytes = 0;
   float* part = nullptr;  // normaliser partials
+  float* zero = nullptr;  // 256 zero bytes for padding taps
 };
 
 namespace {
@@ -173,8 +164,11 @@ void build_plan(clasfv_engine* e) {
   add_param(e, "motion_head.bias", {4});
   add_param(e, "segmentation_head.weight", {2, 64, 1, 1, 1});
   add_param(e, "segmentation_head.bias", {2});
+  // decoder projections: proj[0] is the dual 1x1x1 conv over (stem, layer1) -> P01; proj[1] unused
   const int tap_c[5] = {64, 64, 128, 256, 512};
   for (int i = 0; i < 5; ++i) e->proj[i] = make_conv(PROJ, "", "", tap_c[i], 64, 1, 1, 1, 1, 1, 1, 0, 0, 0);
+  e->proj[0].cin2 = 64;
+  e->proj[0].K = e->proj[0].Kp = 128;
 }
 
 const std::vector<float>& P(clasfv_engine* e, const std::string& n) { return e->params[e->index.at(n)].data; }
@@ -223,7 +217,7 @@ struct Shape5 {
 };
 
 int run_conv(const Conv& c, const float* x, const Shape5& in, float* y, Shape5& out, const float* res, bool relu,
-             hipStream_t s) {
+             hipStream_t s, const float* zero_block, const float* x2 = nullptr) {
   out.n = in.n;
   out.t = (in.t + 2 * c.pt - c.kt) / c.st + 1;
   out.h = (in.h + 2 * c.ph - c.kh) / c.sh + 1;
@@ -242,7 +236,15 @@ int run_conv(const Conv& c, const float* x, const Shape5& in, float* y, Shape5& 
   p.K = c.K, p.Kp = c.Kp;
   p.M = out.n * out.t * out.h * out.w;
   p.relu = relu ? 1 : 0;
-  HIP_TRY(launch_conv(p, c.bn_tile, c.bk, s));
+  p.zero = zero_block;
+  p.x2 = x2;
+  p.Cin2 = c.cin2;
+  int mt = 2, bn = 48;
+  if (c.cin_p % 16 == 0) {
+    static const int force_nt = getenv("CLASFV_CONV_NT") ? atoi(getenv("CLASFV_CONV_NT")) : 0;
+    conv_pick_tile(p.M, c.cout_p, force_nt, &mt, &bn);
+  }
+  HIP_TRY(launch_conv(p, mt, bn, s));
   return CLASFV_OK;
 }
 
@@ -322,6 +324,7 @@ int clasfv_destroy(clasfv_t h) {
   (void)hipFree(h->bh);
   (void)hipFree(h->arena);
   (void)hipFree(h->part);
+  (void)hipFree(h->zero);
   delete h;
   return CLASFV_OK;
 }
@@ -381,16 +384,20 @@ int clasfv_finalize(clasfv_t h) {
   const auto& w1 = P(h, "comb_1_layer.weight");
   const auto& bias1 = P(h, "comb_1_layer.bias");
   std::vector<double> zero(64, 0.0);
-  int off = 0;
+  const int col0[5] = {0, 64, 128, 256, 512};
   for (int i = 0; i < 5; ++i) {
+    if (i == 1) continue;  // folded into the dual proj[0]
     Conv& c = h->proj[i];
     (void)hipFree(c.dw);
     c.dw = nullptr;
-    const int o0 = off;
+    const int o0 = col0[i];
+    const int kin = c.cin + c.cin2;
+    Conv tmp = c;  // upload_conv walks cin: give it the concatenated width
+    tmp.cin = tmp.cin_p = kin;
     int rc = upload_conv(
-        c, [&](int o, int ci, int) { return w1[(size_t)o * 1024 + o0 + ci]; }, s, zero, false);
+        tmp, [&](int o, int ci, int) { return w1[(size_t)o * 1024 + o0 + ci]; }, s, zero, false);
     if (rc) return rc;
-    off += c.cin;
+    c.dw = tmp.dw;
   }
   std::vector<float> b1(64);
   for (int o = 0; o < 64; ++o) b1[o] = (float)(s[o] * (double)bias1[o] + t[o]);
@@ -425,6 +432,10 @@ int clasfv_finalize(clasfv_t h) {
   if (!rc) rc = upload(whf, &h->wh);
   if (!rc) rc = upload(bhf, &h->bh);
   if (rc) return rc;
+  if (!h->zero) {
+    HIP_TRY(hipMalloc(&h->zero, 256));
+    HIP_TRY(hipMemset(h->zero, 0, 256));
+  }
   HIP_TRY(hipDeviceSynchronize());
   h->ready = true;
   return CLASFV_OK;
@@ -458,8 +469,8 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   Shape5 sx{N, T, H, W, 4}, s0, sx0;
   int rc;
   size_t ci = 0;
-  if ((rc = run_conv(h->convs[ci++], buf(XIN), sx, buf(S0), s0, nullptr, true, s))) return rc;
-  if ((rc = run_conv(h->convs[ci++], buf(S0), s0, buf(X0), sx0, nullptr, true, s))) return rc;
+  if ((rc = run_conv(h->convs[ci++], buf(XIN), sx, buf(S0), s0, nullptr, true, s, h->zero))) return rc;
+  if ((rc = run_conv(h->convs[ci++], buf(S0), s0, buf(X0), sx0, nullptr, true, s, h->zero))) return rc;
   const int outs[4][2] = {{L1A, L1}, {L2A, L2}, {L3A, L3}, {L4A, L4}};
   float* cur = buf(X0);
   Shape5 cs = sx0, taps_shape[5];
@@ -474,16 +485,16 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
       const Conv& tp2 = h->convs[ci++];
       const Conv* ds = (ci < h->convs.size() && h->convs[ci].role == DS) ? &h->convs[ci++] : nullptr;
       Shape5 sm, sa, sm2, so, sd;
-      if ((rc = run_conv(sp1, cur, cs, buf(MID), sm, nullptr, true, s))) return rc;
-      if ((rc = run_conv(tp1, buf(MID), sm, buf(TA), sa, nullptr, true, s))) return rc;
-      if ((rc = run_conv(sp2, buf(TA), sa, buf(MID), sm2, nullptr, true, s))) return rc;
+      if ((rc = run_conv(sp1, cur, cs, buf(MID), sm, nullptr, true, s, h->zero))) return rc;
+      if ((rc = run_conv(tp1, buf(MID), sm, buf(TA), sa, nullptr, true, s, h->zero))) return rc;
+      if ((rc = run_conv(sp2, buf(TA), sa, buf(MID), sm2, nullptr, true, s, h->zero))) return rc;
       const float* res = cur;
       if (ds) {
-        if ((rc = run_conv(*ds, cur, cs, buf(DSB), sd, nullptr, false, s))) return rc;
+        if ((rc = run_conv(*ds, cur, cs, buf(DSB), sd, nullptr, false, s, h->zero))) return rc;
         res = buf(DSB);
       }
       float* out = buf(outs[li][b]);
-      if ((rc = run_conv(tp2, buf(MID), sm2, out, so, res, true, s))) return rc;
+      if ((rc = run_conv(tp2, buf(MID), sm2, out, so, res, true, s, h->zero))) return rc;
       cur = out;
       cs = so;
     }
@@ -492,12 +503,11 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   }
   // decoder projections at tap resolution: P01 = W0 f0 + W1 f1, P2..P4
   Shape5 sp;
-  if ((rc = run_conv(h->proj[0], taps[0], taps_shape[0], buf(P01), sp, nullptr, false, s))) return rc;
-  if ((rc = run_conv(h->proj[1], taps[1], taps_shape[1], buf(P01), sp, buf(P01), false, s))) return rc;
+  if ((rc = run_conv(h->proj[0], taps[0], taps_shape[0], buf(P01), sp, nullptr, false, s, h->zero, taps[1]))) return rc;
   Shape5 sp2, sp3, sp4;
-  if ((rc = run_conv(h->proj[2], taps[2], taps_shape[2], buf(PP2), sp2, nullptr, false, s))) return rc;
-  if ((rc = run_conv(h->proj[3], taps[3], taps_shape[3], buf(PP3), sp3, nullptr, false, s))) return rc;
-  if ((rc = run_conv(h->proj[4], taps[4], taps_shape[4], buf(PP4), sp4, nullptr, false, s))) return rc;
+  if ((rc = run_conv(h->proj[2], taps[2], taps_shape[2], buf(PP2), sp2, nullptr, false, s, h->zero))) return rc;
+  if ((rc = run_conv(h->proj[3], taps[3], taps_shape[3], buf(PP3), sp3, nullptr, false, s, h->zero))) return rc;
+  if ((rc = run_conv(h->proj[4], taps[4], taps_shape[4], buf(PP4), sp4, nullptr, false, s, h->zero))) return rc;
 
   DecParams d;
   const Shape5 tsh[4] = {sp, sp2, sp3, sp4};

@@ -71,6 +71,8 @@ def main(argv=None):
     if not args.device.startswith("cuda"):
         sys.exit("error: this engine runs on the GPU (MI355X); use -d cuda")
     dev = torch.device(args.device)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
     torch.cuda.set_device(dev)
 
     from clasfv_amd.echo import compute_ef_using_putative_clips

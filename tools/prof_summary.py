@@ -28,7 +28,7 @@ def forwards(seq, name_of=lambda r: r[0]):
     out, cur = [], []
     for r in seq:
         n = name_of(r)
-        if n.startswith("conv_igemm") or n.startswith("pack_input"):
+        if n.startswith("conv_") or n.startswith("pack_input"):
             cur.append(r)
         elif n.startswith("decoder_kernel"):
             cur.append(r)
