@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--batch-size", type=int, default=32, help="clips per forward call")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--cpu-sample-clips", type=int, default=4)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
     return ap.parse_args()
 
 
@@ -50,10 +51,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:  # rehearsal of the exchange with several ranks on one GPU
+            dist.init_process_group(args.dist_backend)
 
     import clasfv_amd.synthetic as S
     from clasfv_amd import dist as D

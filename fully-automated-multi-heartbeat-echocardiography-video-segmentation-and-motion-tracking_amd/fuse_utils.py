@@ -69,6 +69,9 @@ def to_device_video(video, device):
 
 def build_clips(video_dev, table, interpolate_last=True):
     """(n,3,32,H,W) clips on the device for a [(shift, first_frame)] table."""
+    if video_dev.dim() != 4 or video_dev.shape[0] != 3:
+        raise ValueError(f"expected a (3,T,H,W) video, got {tuple(video_dev.shape)}")
+    video_dev = video_dev.to(torch.float32).contiguous()  # the ABI takes dense row-major buffers
     _, t, h, w = video_dev.shape
     tab = torch.tensor(np.asarray(table, np.int32).reshape(-1), device=video_dev.device)
     clips = torch.empty((len(table), 3, CLIP, h, w), device=video_dev.device, dtype=torch.float32)
@@ -102,6 +105,7 @@ def run_model(model, clips, batch_size=None):
 
 
 def fuse_votes(labels, step, fuse_method="simple"):
+    labels = labels.to(torch.uint8).contiguous()
     k, t, h, w = labels.shape
     method = FUSE_METHODS.get(fuse_method.lower())
     if method is None:
@@ -141,6 +145,7 @@ def segment_a_video_with_fusion_device(video, model, interpolate_last=True, step
 def pass_labels(logits, clip0, t, step, interpolate_last=True):
     """(K,T,H,W) uint8 labels of the K shifted passes (softmax -> resample -> argmax)."""
     k = len(clip0)
+    logits = logits.to(torch.float32).contiguous()
     h, w = logits.shape[-2:]
     labels = torch.empty((k, t, h, w), device=logits.device, dtype=torch.uint8)
     ptr, keep = ctypes_int32_array(clip0)

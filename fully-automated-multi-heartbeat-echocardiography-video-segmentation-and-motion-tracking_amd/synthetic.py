@@ -43,4 +43,4 @@ def echo_video_uint8(T=200, H=112, W=112, seed=0, period=50):
 
 def echo_video(T=200, H=112, W=112, seed=0, period=50):
     """(3,T,H,W) float32 video after the CLI's transpose (motion_segment.py:96), not normalised."""
-    return echo_video_uint8(T, H, W, seed, period).transpose(3, 0, 1, 2).astype(np.float32)
+    return np.ascontiguousarray(echo_video_uint8(T, H, W, seed, period).transpose(3, 0, 1, 2), dtype=np.float32)

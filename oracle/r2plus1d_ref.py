@@ -75,6 +75,59 @@ def head(sd, taps):
     return seg, mot
 
 
+def _lerp_frames(t, t_out):
+    """align_corners=True linear resampling of dim 2 to t_out frames."""
+    t_in = t.shape[2]
+    if t_in == t_out:
+        return t
+    scale = (t_in - 1) / (t_out - 1) if t_out > 1 else 0.0
+    idx = torch.arange(t_out, dtype=torch.float32) * torch.tensor(scale, dtype=torch.float32)
+    i0 = torch.clamp(idx.floor().long(), max=t_in - 1)
+    lam = (idx - i0.float()).clamp(0, 1)
+    i1 = torch.clamp(i0 + 1, max=t_in - 1)
+    lam = lam.view(1, 1, -1, 1, 1)
+    return t[:, :, i0] * (1 - lam) + t[:, :, i1] * lam
+
+
+@torch.no_grad()
+def forward_chunked(sd, x, frames_per_chunk=4):
+    """Same function as ``forward`` for large clips (e.g. BASELINE config[3], 64x224x224, whose
+    as-written concat is 13 GB): the five trilinear align_corners=True upsamplings are evaluated
+    separably (time, then F.interpolate bilinear over H, W) for a few output frames at a time and
+    the 1x1x1 head is applied per chunk. Equal to ``forward`` up to fp32 rounding."""
+    if not torch.is_tensor(x):
+        x = torch.from_numpy(x)
+    x = x.float()
+    taps = backbone(sd, x)
+    n, _, t, h, w = x.shape
+    segs, mots = [], []
+    for t0 in range(0, t, frames_per_chunk):
+        t1 = min(t, t0 + frames_per_chunk)
+        ups = []
+        for tap in taps:
+            lt = _lerp_frames(tap, t)[:, :, t0:t1]
+            c, k = lt.shape[1], lt.shape[2]
+            sp = F.interpolate(lt.permute(0, 2, 1, 3, 4).reshape(n * k, c, lt.shape[3], lt.shape[4]), size=(h, w),
+                               mode="bilinear", align_corners=True)
+            ups.append(sp.reshape(n, k, c, h, w).permute(0, 2, 1, 3, 4))
+        s_, m_ = head_from_cat(sd, torch.cat(ups, 1))
+        segs.append(s_)
+        mots.append(m_)
+    return torch.cat(segs, 2), torch.cat(mots, 2)
+
+
+def head_from_cat(sd, cat):
+    h = F.conv3d(cat, _t(sd, "comb_1_layer.weight"), _t(sd, "comb_1_layer.bias"))
+    h = F.relu(F.batch_norm(h, _t(sd, "comb_batch_norm_1.running_mean"), _t(sd, "comb_batch_norm_1.running_var"),
+                            _t(sd, "comb_batch_norm_1.weight"), _t(sd, "comb_batch_norm_1.bias"), False, 0.0, _EPS))
+    h = F.conv3d(h, _t(sd, "comb_2_layer.weight"), _t(sd, "comb_2_layer.bias"))
+    h = F.relu(F.batch_norm(h, _t(sd, "comb_batch_norm_2.running_mean"), _t(sd, "comb_batch_norm_2.running_var"),
+                            _t(sd, "comb_batch_norm_2.weight"), _t(sd, "comb_batch_norm_2.bias"), False, 0.0, _EPS))
+    seg = F.conv3d(h, _t(sd, "segmentation_head.weight"), _t(sd, "segmentation_head.bias"))
+    mot = torch.tanh(F.conv3d(h, _t(sd, "motion_head.weight"), _t(sd, "motion_head.bias")))
+    return seg, mot
+
+
 @torch.no_grad()
 def forward(sd, x):
     """x: (N,3,T,H,W) float32 CPU tensor -> (seg_logits (N,2,T,H,W), motion (N,4,T,H,W))."""

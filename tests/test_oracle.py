@@ -131,3 +131,13 @@ def test_simple_vote_properties():
     np.testing.assert_array_equal(fuse_ref.simple_vote([a, a, a]), a)
     np.testing.assert_array_equal(fuse_ref.simple_vote([a, a, 1 - a]), a)
     np.testing.assert_array_equal(fuse_ref.majority_vote([a, 1 - a]), np.zeros_like(a))
+
+
+def test_chunked_oracle_equals_as_written(synthetic_sd):
+    """forward_chunked (used for 64x224x224 clips) is the same function as the as-written head."""
+    rng = np.random.default_rng(12)
+    x = rng.uniform(0, 1, (1, 3, 16, 48, 64)).astype(np.float32)
+    s1, m1 = r2plus1d_ref.forward(synthetic_sd, x)
+    s2, m2 = r2plus1d_ref.forward_chunked(synthetic_sd, x, frames_per_chunk=3)
+    np.testing.assert_allclose(s2.numpy(), s1.numpy(), atol=2e-5)
+    np.testing.assert_allclose(m2.numpy(), m1.numpy(), atol=1e-6)
