@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--cpu-sample-clips", type=int, default=4)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"], help="encoder compute dtype of the headline run")
+    ap.add_argument("--extra-bf16", type=int, default=1,
+                    help="also time the bf16 path (BASELINE config[4]) on the same workload; reported as 'bf16'")
     return ap.parse_args()
 
 
@@ -65,7 +68,7 @@ def main():
     from clasfv_amd.model import R2plus1D_18_MotionNet
     from clasfv_amd.preprocess import zeroone_normalize_
 
-    model = R2plus1D_18_MotionNet(pretrained=False)
+    model = R2plus1D_18_MotionNet(pretrained=False, dtype=args.dtype)
     n_videos = args.videos_per_gpu * world
     videos = []
     for v in range(n_videos):  # synthetic EchoNet-style videos, normalised on the device (not timed)
@@ -127,6 +130,39 @@ def main():
     if rank == 0 and world == 1 and args.cpu_baseline:
         cpu, dice = cpu_baseline(args, S, model)
 
+    bf16 = None
+    if args.extra_bf16 and args.dtype == "fp32":
+        # same workload with the bf16 encoder; Dice of its fused masks against this run's fp32 masks
+        ref_masks = {k: v.clone() for k, v in out.items()}
+        model.set_compute_dtype("bf16")
+        for _ in range(args.warmup):
+            step()
+        fwd_events.clear()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out16 = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt16 = time.perf_counter() - t0
+        t = torch.tensor([dt16], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt16 = float(t.item())
+        f16_ms = sum(a.elapsed_time(b) for a, b, _ in fwd_events)
+        f16_clips = sum(n for _, _, n in fwd_events)
+        from clasfv_amd.echo import categorical_dice
+        d16 = [1.0 - categorical_dice(out16[k].cpu().numpy(), ref_masks[k].cpu().numpy(), 1) for k in out16]
+        bf16 = {"value": round(clips_per_step * args.steps / dt16, 3), "unit": "clips/s",
+                "ms_per_step": round(dt16 / args.steps * 1e3, 3),
+                "forward_ms_per_clip": round(f16_ms / max(f16_clips, 1), 4),
+                "dice_delta_vs_fp32_fused_masks": round(float(max(d16)) if d16 else 0.0, 6),
+                "note": "BASELINE config[4]: bf16 activations/weights, fp32 accumulate, fp32 decoder head; "
+                        "Dice tolerance 1e-2"}
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -155,6 +191,7 @@ def main():
                          "gflop_per_clip": GFLOP_PER_CLIP, "forward_ms_per_clip": round(fwd_ms / max(fwd_clips, 1), 4)},
             "cpu_baseline": cpu,
             "dice_delta_vs_cpu": dice,
+            "bf16": bf16,
             "lv_fraction": round(lv_frac, 4),
         }
         print(json.dumps(line), flush=True)

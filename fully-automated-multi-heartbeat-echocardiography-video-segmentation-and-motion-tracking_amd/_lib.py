@@ -22,6 +22,8 @@ SIGNATURES = {
     "clasfv_finalize": (c_int, [_P]),
     "clasfv_forward": (c_int, [_P, _P, c_int, c_int, c_int, c_int, _P, _P, _P]),
     "clasfv_workspace_bytes": (c_int64, [_P]),
+    "clasfv_set_compute_dtype": (c_int, [_P, c_int]),
+    "clasfv_get_compute_dtype": (c_int, [_P]),
     "clasfv_build_clips": (c_int, [_P, c_int, c_int, c_int, _P, c_int, c_int, _P, _P]),
     "clasfv_pass_labels": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, _P]),
     "clasfv_fuse_votes": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, _P, _P]),
@@ -30,6 +32,7 @@ SIGNATURES = {
 }
 
 FUSE_MAJORITY, FUSE_SIMPLE = 0, 1
+DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
 _lib = None
 
 

@@ -10,18 +10,20 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 //   m = ((n*To + to)*Ho + ho)*Wo + wo            (output voxel)
 //   k = ((kt*KH + kh)*KW + kw)*Cin + c           (tap-major, channel-minor)
 struct ConvParams {
-  const float* x;     // [N][Ti][Hi][Wi][Cin]
-  const float* w;     // [Cout_alloc][Kp], zero padded
+  const void* x;      // [N][Ti][Hi][Wi][Cin], fp32 or bf16 (in_bf16)
+  const void* w;      // [Cout_alloc][Kp], zero padded, same dtype as x
   const float* bias;  // [Cout_alloc] or nullptr
-  const float* res;   // [M][Cout] or nullptr (may alias y)
-  float* y;           // [M][Cout]
+  const void* res;    // [M][Cout] or nullptr (may alias y), dtype of y
+  void* y;            // [M][Cout], fp32 or bf16 (out_bf16)
   int N, Ti, Hi, Wi, Cin;
   int To, Ho, Wo, Cout;
   int KT, KH, KW, st, sh, sw, pt, ph, pw;
   int K, Kp, M, relu;
-  const float* zero;  // >= 16 zero bytes (source of padding taps for the LDS-DMA path)
-  const float* x2;    // optional second input of a 1x1x1 conv (same voxels), K columns after x's
+  const void* zero;   // >= 16 zero bytes (source of padding taps for the LDS-DMA path)
+  const void* x2;     // optional second input of a 1x1x1 conv (same voxels), K columns after x's
   int Cin2;
+  int stem;           // fp32 4-channel input (3 + pad): register-staged kernel, per-float4 tap decode
+  int in_bf16, out_bf16;
 };
 
 // Decoder tap: low-resolution projection P_i = (s1 * W_i) . f_i, channels-last with 64 channels.

@@ -49,10 +49,19 @@ struct Param {
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
-int pad_channels(int c) {
+// Padded channel count of an activation tensor: a multiple of the K step (16 fp32 / 32 bf16
+// channels) whose 16-channel count has a divisor in {9,8,6,5,4,3} (a legal N tile). The network
+// input keeps 3 + 1 fp32 channels (stem kernel).
+int pad_channels(int c, bool bf16) {
   if (c == 3) return 4;
-  int cp = round_up(c, 16);
-  if (cp % 64 != 0 && cp % 48 != 0) cp = round_up(cp, 48);
+  const int step = bf16 ? 32 : 16;
+  int cp = round_up(c, step);
+  auto ok = [](int cp_) {
+    for (int nt : {9, 8, 6, 5, 4, 3})
+      if ((cp_ / 16) % nt == 0) return true;
+    return false;
+  };
+  while (!ok(cp)) cp += step;
   return cp;
 }
 
@@ -65,9 +74,22 @@ struct Conv {
   int kt, kh, kw, st, sh, sw, pt, ph, pw;
   int K, Kp, cout_alloc;
   int cin2 = 0;  // second input of a dual 1x1x1 conv (decoder P01 = W0 f_stem + W1 f_layer1)
-  float* dw = nullptr;
-  float* db = nullptr;
+  int stem = 0, in_bf16 = 0, out_bf16 = 0;
+  void* dw = nullptr;   // weights, dtype of the conv's input
+  float* db = nullptr;  // folded-BN bias (fp32)
 };
+
+// Channel padding, K extent and dtypes of one conv for the engine's compute dtype.
+void layout_conv(Conv& c, bool bf16) {
+  c.stem = (c.role == STEM_S);
+  c.in_bf16 = bf16 && !c.stem;
+  c.out_bf16 = bf16 && c.role != PROJ;
+  c.cin_p = pad_channels(c.cin, bf16);
+  c.cout_p = c.role == PROJ ? c.cout : pad_channels(c.cout, bf16);
+  c.K = c.kt * c.kh * c.kw * c.cin_p + c.cin2;
+  c.Kp = round_up(c.K, c.in_bf16 ? 32 : 16);
+  c.cout_alloc = c.cout_p;  // every tile width used divides cout_p
+}
 
 Conv make_conv(Role role, const std::string& w, const std::string& bn, int cin, int cout, int kt, int kh, int kw,
                int st, int sh, int sw, int pt, int ph, int pw) {
@@ -77,12 +99,8 @@ Conv make_conv(Role role, const std::string& w, const std::string& bn, int cin, 
   c.bn = bn;
   c.cin = cin;
   c.cout = cout;
-  c.cin_p = pad_channels(cin);
-  c.cout_p = pad_channels(cout);
   c.kt = kt, c.kh = kh, c.kw = kw, c.st = st, c.sh = sh, c.sw = sw, c.pt = pt, c.ph = ph, c.pw = pw;
-  c.K = kt * kh * kw * c.cin_p;
-  c.Kp = round_up(c.K, 16);
-  c.cout_alloc = c.cout_p;  // every tile width used divides cout_p
+  layout_conv(c, false);
   return c;
 }
 
@@ -98,6 +116,7 @@ struct clasfv_engine {
   Conv proj[5];             // decoder projections (stem, layer1..4) -> 64 channels
   float *b1 = nullptr, *w2 = nullptr, *b2 = nullptr, *wh = nullptr, *bh = nullptr;
   bool ready = false;
+  int dtype = CLASFV_DTYPE_FP32;  // compute dtype of the encoder convs
   // workspace arena
   char* arena = nullptr;
   size_t arena_bytes = 0;
@@ -168,7 +187,7 @@ void build_plan(clasfv_engine* e) {
   const int tap_c[5] = {64, 64, 128, 256, 512};
   for (int i = 0; i < 5; ++i) e->proj[i] = make_conv(PROJ, "", "", tap_c[i], 64, 1, 1, 1, 1, 1, 1, 0, 0, 0);
   e->proj[0].cin2 = 64;
-  e->proj[0].K = e->proj[0].Kp = 128;
+  layout_conv(e->proj[0], false);
 }
 
 const std::vector<float>& P(clasfv_engine* e, const std::string& n) { return e->params[e->index.at(n)].data; }
@@ -192,6 +211,22 @@ int upload(const std::vector<float>& h, float** d) {
   return CLASFV_OK;
 }
 
+// float -> bf16 bits, round to nearest even (weights are finite).
+uint16_t to_bf16(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  u += 0x7FFF + ((u >> 16) & 1);
+  return (uint16_t)(u >> 16);
+}
+
+int upload_bf16(const std::vector<float>& h, void** d) {
+  std::vector<uint16_t> b(h.size());
+  for (size_t i = 0; i < h.size(); ++i) b[i] = to_bf16(h[i]);
+  HIP_TRY(hipMalloc(d, b.size() * sizeof(uint16_t)));
+  HIP_TRY(hipMemcpy(*d, b.data(), b.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  return CLASFV_OK;
+}
+
 // Folded, padded [cout_alloc][Kp] weight image of one conv. `wsrc(o, c, tap)` returns the raw weight.
 template <class F>
 int upload_conv(Conv& c, F wsrc, const std::vector<double>& scale, const std::vector<double>& shift, bool has_bias) {
@@ -201,7 +236,7 @@ int upload_conv(Conv& c, F wsrc, const std::vector<double>& scale, const std::ve
     for (int tap = 0; tap < taps; ++tap)
       for (int ci = 0; ci < c.cin; ++ci)
         w[(size_t)o * c.Kp + (size_t)tap * c.cin_p + ci] = (float)((double)wsrc(o, ci, tap) * scale[o]);
-  int rc = upload(w, &c.dw);
+  int rc = c.in_bf16 ? upload_bf16(w, &c.dw) : upload(w, reinterpret_cast<float**>(&c.dw));
   if (rc) return rc;
   if (has_bias) {
     std::vector<float> b(c.cout_alloc, 0.f);
@@ -216,8 +251,8 @@ struct Shape5 {
   size_t numel() const { return (size_t)n * t * h * w * c; }
 };
 
-int run_conv(const Conv& c, const float* x, const Shape5& in, float* y, Shape5& out, const float* res, bool relu,
-             hipStream_t s, const float* zero_block, const float* x2 = nullptr) {
+int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
+             hipStream_t s, const void* zero_block, const void* x2 = nullptr) {
   out.n = in.n;
   out.t = (in.t + 2 * c.pt - c.kt) / c.st + 1;
   out.h = (in.h + 2 * c.ph - c.kh) / c.sh + 1;
@@ -239,8 +274,11 @@ int run_conv(const Conv& c, const float* x, const Shape5& in, float* y, Shape5& 
   p.zero = zero_block;
   p.x2 = x2;
   p.Cin2 = c.cin2;
-  int mt = 2, bn = 48;
-  if (c.cin_p % 16 == 0) {
+  p.stem = c.stem;
+  p.in_bf16 = c.in_bf16;
+  p.out_bf16 = c.out_bf16;
+  int mt = 2, bn = c.cout_p;  // stem: one N tile (48 fp32 / 64 bf16 channels)
+  if (!c.stem) {
     static const int force_nt = getenv("CLASFV_CONV_NT") ? atoi(getenv("CLASFV_CONV_NT")) : 0;
     conv_pick_tile(p.M, c.cout_p, force_nt, &mt, &bn);
   }
@@ -366,6 +404,9 @@ int clasfv_finalize(clasfv_t h) {
     if (!p.loaded && p.name.find(".fc.") == std::string::npos)
       return fail(CLASFV_ENOTREADY, "parameter not loaded: " + p.name);
   HIP_TRY(hipSetDevice(h->device));
+  const bool bf16 = h->dtype == CLASFV_DTYPE_BF16;
+  for (auto& c : h->convs) layout_conv(c, bf16);
+  for (auto& c : h->proj) layout_conv(c, bf16);
   std::vector<double> s, t;
   for (auto& c : h->convs) {
     (void)hipFree(c.dw);
@@ -443,6 +484,18 @@ int clasfv_finalize(clasfv_t h) {
 
 int64_t clasfv_workspace_bytes(clasfv_t h) { return h ? (int64_t)h->arena_bytes : 0; }
 
+int clasfv_set_compute_dtype(clasfv_t h, int dtype) {
+  if (!h) return fail(CLASFV_EINVAL, "null handle");
+  if (dtype != CLASFV_DTYPE_FP32 && dtype != CLASFV_DTYPE_BF16) return fail(CLASFV_EINVAL, "unknown dtype");
+  if (dtype != h->dtype) {
+    h->dtype = dtype;
+    h->ready = false;  // weights must be re-laid-out: call clasfv_finalize again
+  }
+  return CLASFV_OK;
+}
+
+int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; }
+
 int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float* seg, float* mot, void* stream) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
   if (!h->ready) return fail(CLASFV_ENOTREADY, "clasfv_finalize has not been called");
@@ -463,18 +516,18 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
     HIP_TRY(hipMalloc(&h->arena, L.total));
     h->arena_bytes = L.total;
   }
-  auto buf = [&](int b) { return reinterpret_cast<float*>(h->arena + L.off[b]); };
+  auto buf = [&](int b) { return reinterpret_cast<void*>(h->arena + L.off[b]); };
 
-  HIP_TRY(launch_pack_input(x, buf(XIN), N, T, H * W, s));
+  HIP_TRY(launch_pack_input(x, reinterpret_cast<float*>(buf(XIN)), N, T, H * W, s));
   Shape5 sx{N, T, H, W, 4}, s0, sx0;
   int rc;
   size_t ci = 0;
   if ((rc = run_conv(h->convs[ci++], buf(XIN), sx, buf(S0), s0, nullptr, true, s, h->zero))) return rc;
   if ((rc = run_conv(h->convs[ci++], buf(S0), s0, buf(X0), sx0, nullptr, true, s, h->zero))) return rc;
   const int outs[4][2] = {{L1A, L1}, {L2A, L2}, {L3A, L3}, {L4A, L4}};
-  float* cur = buf(X0);
+  void* cur = buf(X0);
   Shape5 cs = sx0, taps_shape[5];
-  float* taps[5];
+  void* taps[5];
   taps[0] = cur;
   taps_shape[0] = cs;
   for (int li = 0; li < 4; ++li) {
@@ -488,12 +541,12 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
       if ((rc = run_conv(sp1, cur, cs, buf(MID), sm, nullptr, true, s, h->zero))) return rc;
       if ((rc = run_conv(tp1, buf(MID), sm, buf(TA), sa, nullptr, true, s, h->zero))) return rc;
       if ((rc = run_conv(sp2, buf(TA), sa, buf(MID), sm2, nullptr, true, s, h->zero))) return rc;
-      const float* res = cur;
+      const void* res = cur;
       if (ds) {
         if ((rc = run_conv(*ds, cur, cs, buf(DSB), sd, nullptr, false, s, h->zero))) return rc;
         res = buf(DSB);
       }
-      float* out = buf(outs[li][b]);
+      void* out = buf(outs[li][b]);
       if ((rc = run_conv(tp2, buf(MID), sm2, out, so, res, true, s, h->zero))) return rc;
       cur = out;
       cs = so;
@@ -513,7 +566,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   const Shape5 tsh[4] = {sp, sp2, sp3, sp4};
   const int tb[4] = {P01, PP2, PP3, PP4};
   for (int i = 0; i < 4; ++i) {
-    d.tap[i].p = buf(tb[i]);
+    d.tap[i].p = reinterpret_cast<const float*>(buf(tb[i]));
     d.tap[i].T = tsh[i].t;
     d.tap[i].H = tsh[i].h;
     d.tap[i].W = tsh[i].w;

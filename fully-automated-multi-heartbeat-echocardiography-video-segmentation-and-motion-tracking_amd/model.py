@@ -28,7 +28,7 @@ from .weights import DEFAULT_SEED, synthetic_state_dict
 class Engine:
     """Owns one clasfv handle (weights + workspace) on one HIP device."""
 
-    def __init__(self, device=None):
+    def __init__(self, device=None, dtype="fp32"):
         if not torch.cuda.is_available():
             raise RuntimeError("CLAS-FV engine requires a HIP (ROCm) GPU; none is visible")
         self.lib = _lib.load()
@@ -37,6 +37,14 @@ class Engine:
         h = ctypes.c_void_p()
         _lib.check(self.lib.clasfv_create(self.device.index, ctypes.byref(h)), "clasfv_create")
         self.h = h
+        self.set_dtype(dtype)
+
+    def set_dtype(self, dtype):
+        """'fp32' (default, reference precision) or 'bf16' (BASELINE config[4]); re-load weights after."""
+        if dtype not in _lib.DTYPES:
+            raise ValueError(f"dtype must be one of {sorted(_lib.DTYPES)}")
+        _lib.check(self.lib.clasfv_set_compute_dtype(self.h, _lib.DTYPES[dtype]), "clasfv_set_compute_dtype")
+        self.dtype = "bf16" if _lib.DTYPES[dtype] == 1 else "fp32"
 
     def __del__(self):
         try:
@@ -75,17 +83,23 @@ class Engine:
 class R2plus1D_18_MotionNet(nn.Module):
     """HIP-backed drop-in for the reference model (inference)."""
 
-    def __init__(self, pretrained=True, output_channels=4, device=None, seed=DEFAULT_SEED):
+    def __init__(self, pretrained=True, output_channels=4, device=None, seed=DEFAULT_SEED, dtype="fp32"):
         super().__init__()
         if output_channels != 4:
             raise ValueError("the motion head has 4 channels [fwd x, fwd y, bwd x, bwd y]")
         if pretrained:
             warnings.warn("pretrained=True: Kinetics weights cannot be downloaded offline; using seeded synthetic "
                           "weights (load a checkpoint with load_state_dict)", stacklevel=2)
-        self.engine = Engine(device)
+        self.engine = Engine(device, dtype)
         self._state = OrderedDict()
         self._params = None
         self._load(synthetic_state_dict(seed))
+
+    def set_compute_dtype(self, dtype):
+        """Switch the encoder between exact fp32 and bf16 (fp32 accumulation) and re-upload weights."""
+        self.engine.set_dtype(dtype)
+        self.engine.load(self._state)
+        return self
 
     # ---- state dict ------------------------------------------------------------------------------
     def _load(self, sd):

@@ -41,6 +41,7 @@ enum {
 };
 
 enum { CLASFV_FUSE_MAJORITY = 0, CLASFV_FUSE_SIMPLE = 1 };
+enum { CLASFV_DTYPE_FP32 = 0, CLASFV_DTYPE_BF16 = 1 };
 
 typedef struct clasfv_engine* clasfv_t;
 
@@ -64,6 +65,12 @@ int clasfv_forward(clasfv_t h, const float* x_dev, int N, int T, int H, int W, f
                    float* motion_dev, void* stream);
 /* Bytes of library workspace currently held (activation arena; grows to the largest N*T*H*W seen). */
 int64_t clasfv_workspace_bytes(clasfv_t h);
+/* Compute dtype of the encoder: CLASFV_DTYPE_FP32 (default; exact-fp32 MFMA, the reference's
+ * precision) or CLASFV_DTYPE_BF16 (bf16 activations/weights, fp32 accumulation; BASELINE config[4],
+ * Dice tolerance 1e-2). The decoder head runs in fp32 either way. A change takes effect at the next
+ * clasfv_finalize. */
+int clasfv_set_compute_dtype(clasfv_t h, int dtype);
+int clasfv_get_compute_dtype(clasfv_t h);
 
 /* ---- clip plumbing: replaces src/fuse_utils.py:16-100 ----------------------------------------- */
 /* Build n clips (n,3,32,H,W) from the normalised video (3,T,H,W). Clip i is frames

@@ -299,3 +299,26 @@ def test_wrappers_accept_non_contiguous_inputs(model):
     assert torch.equal(a, b)
     assert torch.equal(FU.segment_a_video_with_fusion_device(strided, fake_model, num_clips=3),
                        FU.segment_a_video_with_fusion_device(v, fake_model, num_clips=3))
+
+
+def test_forward_bf16_vs_reference_golden_config4_tolerance(model):
+    """BASELINE config[4]: bf16 activations/weights with fp32 accumulation, Dice tolerance 1e-2."""
+    import clasfv_amd.synthetic as S
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    g = golden("model_forward.npz")
+    v = fuse_ref.zeroone_normalizer(S.echo_video(int(g["big_T"]), seed=int(g["big_video_seed"])))
+    s = int(g["big_start"])
+    m16 = R2plus1D_18_MotionNet(pretrained=False, dtype="bf16")
+    seg, mot = m16(torch.from_numpy(np.ascontiguousarray(v[None, :, s:s + 32])))
+    seg = seg.cpu().numpy()
+    lab = (seg[0, 1] > seg[0, 0]).ravel()
+    ref = np.unpackbits(g["big_label_bits"])[: lab.size].astype(bool)
+    assert dice_delta(lab, ref) <= 1e-2
+    idx = g["big_idx"]
+    err = np.abs(seg[0, 1].ravel()[idx] - g["big_seg1"])
+    assert np.median(err) < 0.05 and err.max() < 0.5
+    # switching back to fp32 restores the exact path
+    m16.set_compute_dtype("fp32")
+    s32, _ = m16(torch.from_numpy(np.ascontiguousarray(v[None, :, s:s + 32])))
+    s_ref, _ = model(torch.from_numpy(np.ascontiguousarray(v[None, :, s:s + 32])))
+    assert torch.equal(s32, s_ref)
