@@ -28,6 +28,11 @@ constexpr int kFrames[4] = {1, 2, 2, 2};
 constexpr int kPixOff[5] = {0, 1 * 6 * 10, 1 * 6 * 10 + 2 * 4 * 6, 1 * 6 * 10 + 2 * 4 * 6 + 2 * 3 * 4,
                             1 * 6 * 10 + 2 * 4 * 6 + 2 * 3 * 4 + 2 * 3 * 3};
 constexpr int STAGE_FLOATS = kPixOff[4] * PIX;
+// per-thread 16-byte staging loads per tap: ceil(frames * rows * cols * 16 / 256)
+constexpr int kLoads[4] = {(1 * 6 * 10 * 16 + 255) / 256, (2 * 4 * 6 * 16 + 255) / 256, (2 * 3 * 4 * 16 + 255) / 256,
+                           (2 * 3 * 3 * 16 + 255) / 256};
+constexpr int kLoadOff[4] = {0, kLoads[0], kLoads[0] + kLoads[1], kLoads[0] + kLoads[1] + kLoads[2]};
+constexpr int kLoadsTotal = kLoads[0] + kLoads[1] + kLoads[2] + kLoads[3];
 
 struct Win {
   int t0, t1, nf, r0, nr, c0, nc;
@@ -42,7 +47,7 @@ __device__ inline void src_index(float s, int dst, int in, int& i0, int& i1, flo
   l0 = 1.f - l1;
 }
 
-__global__ __launch_bounds__(256, 4) void decoder_kernel(DecParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void decoder_kernel(DecParams p) {
   extern __shared__ __align__(16) float smem[];
   float* stage = smem;  // STAGE_FLOATS
 
@@ -77,19 +82,36 @@ __global__ __launch_bounds__(256, 4) void decoder_kernel(DecParams p) {
     w.nc = min(c1 - c0 + 1, kMaxCols[i]);
     win[i] = w;
   }
+  // All staging loads are issued before the first LDS write (fixed per-tap trip counts, predicated),
+  // so one block waits for one HBM/L2 latency instead of one per 16-byte chunk.
+  f32x4 buf[kLoadsTotal];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const DecTap& tp = p.tap[i];
     const Win& w = win[i];
     const int total = w.nf * w.nr * w.nc * 16;
+#pragma unroll
+    for (int k = 0; k < kLoads[i]; ++k) {
+      const int e = tid + 256 * k;
+      if (e < total) {
+        const int c4 = e & 15, px = e >> 4;
+        const int cc = px % w.nc, tmp = px / w.nc;
+        const int rr = tmp % w.nr, ff = tmp / w.nr;
+        const int tf = ff ? w.t1 : w.t0;
+        const size_t off = ((((size_t)n * tp.T + tf) * tp.H + (w.r0 + rr)) * tp.W + (w.c0 + cc)) * 64 + c4 * 4;
+        buf[kLoadOff[i] + k] = *reinterpret_cast<const f32x4*>(tp.p + off);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const Win& w = win[i];
+    const int total = w.nf * w.nr * w.nc * 16;
     float* dst = stage + kPixOff[i] * PIX;
-    for (int e = tid; e < total; e += 256) {
-      const int c4 = e & 15, px = e >> 4;
-      const int cc = px % w.nc, tmp = px / w.nc;
-      const int rr = tmp % w.nr, ff = tmp / w.nr;
-      const int tf = ff ? w.t1 : w.t0;
-      const size_t off = ((((size_t)n * tp.T + tf) * tp.H + (w.r0 + rr)) * tp.W + (w.c0 + cc)) * 64 + c4 * 4;
-      *reinterpret_cast<f32x4*>(dst + px * PIX + c4 * 4) = *reinterpret_cast<const f32x4*>(tp.p + off);
+#pragma unroll
+    for (int k = 0; k < kLoads[i]; ++k) {
+      const int e = tid + 256 * k;
+      if (e < total) *reinterpret_cast<f32x4*>(dst + (e >> 4) * PIX + (e & 15) * 4) = buf[kLoadOff[i] + k];
     }
   }
   __syncthreads();
@@ -147,14 +169,18 @@ __global__ __launch_bounds__(256, 4) void decoder_kernel(DecParams p) {
       for (int j = 0; j < 4; ++j) h1[c][j] = fmaxf(h1[c][j], 0.f);
 
     // 3. h2^T[n][v] = sum_k W2[n][k] h1[v][k]; MFMA j of lane group q covers k = 16c + 4q + j
-    f32x4 acc[4];
+    // (W2 rows of the next 16-channel tile are prefetched while the current one runs on MFMA)
+    f32x4 acc[4], wa[4], wn[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wa[c] = *reinterpret_cast<const f32x4*>(p.w2 + l16 * 64 + 16 * c + 4 * q);
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 wa[4];
+      if (nt < 3) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        wa[c] = *reinterpret_cast<const f32x4*>(p.w2 + (nt * 16 + l16) * 64 + 16 * c + 4 * q);
+        for (int c = 0; c < 4; ++c)
+          wn[c] = *reinterpret_cast<const f32x4*>(p.w2 + ((nt + 1) * 16 + l16) * 64 + 16 * c + 4 * q);
+      }
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -164,6 +190,8 @@ __global__ __launch_bounds__(256, 4) void decoder_kernel(DecParams p) {
       const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[nt][r] = fmaxf(acc[nt][r] + bb[r], 0.f);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wa[c] = wn[c];
     }
     // 4. heads^T[co][v] = sum_k Wh[co][k] h2^T[k][v]; the accumulator layout is the B operand
     f32x4 out = f32x4{0.f, 0.f, 0.f, 0.f};

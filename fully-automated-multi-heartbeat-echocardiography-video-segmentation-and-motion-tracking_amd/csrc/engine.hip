@@ -75,9 +75,18 @@ struct Conv {
   int K, Kp, cout_alloc;
   int cin2 = 0;  // second input of a dual 1x1x1 conv (decoder P01 = W0 f_stem + W1 f_layer1)
   int stem = 0, in_bf16 = 0, out_bf16 = 0;
-  void* dw = nullptr;   // weights, dtype of the conv's input
-  float* db = nullptr;  // folded-BN bias (fp32)
+  void* dw = nullptr;     // weights, dtype of the conv's input
+  float* db = nullptr;    // folded-BN bias (fp32)
+  float* dwino = nullptr;  // Winograd F(2x2,3x3) transformed weights (fp32 stride-1 1x3x3 convs)
 };
+
+// fp32 stride-1 1x3x3 convs run on the fused Winograd kernel unless CLASFV_WINOGRAD=0.
+bool use_wino(const Conv& c, bool bf16) {
+  const char* e = getenv("CLASFV_WINOGRAD");
+  if (e && e[0] == '0') return false;
+  return !bf16 && (c.role == SP1 || c.role == SP2) && c.kt == 1 && c.kh == 3 && c.kw == 3 && c.sh == 1 &&
+         c.sw == 1 && c.cin_p % 16 == 0 && c.cout_p % 48 == 0;
+}
 
 // Channel padding, K extent and dtypes of one conv for the engine's compute dtype.
 void layout_conv(Conv& c, bool bf16) {
@@ -277,6 +286,14 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   p.stem = c.stem;
   p.in_bf16 = c.in_bf16;
   p.out_bf16 = c.out_bf16;
+  if (c.dwino) {
+    p.w = c.dwino;
+    if (wino_supported(p)) {
+      HIP_TRY(launch_wino(p, s));
+      return CLASFV_OK;
+    }
+    p.w = c.dw;
+  }
   int mt = 2, bn = c.cout_p;  // stem: one N tile (48 fp32 / 64 bf16 channels)
   if (!c.stem) {
     static const int force_nt = getenv("CLASFV_CONV_NT") ? atoi(getenv("CLASFV_CONV_NT")) : 0;
@@ -353,6 +370,7 @@ int clasfv_destroy(clasfv_t h) {
   for (auto& c : h->convs) {
     (void)hipFree(c.dw);
     (void)hipFree(c.db);
+    (void)hipFree(c.dwino);
   }
   for (auto& c : h->proj) (void)hipFree(c.dw);
   (void)hipFree(h->b1);
@@ -411,7 +429,9 @@ int clasfv_finalize(clasfv_t h) {
   for (auto& c : h->convs) {
     (void)hipFree(c.dw);
     (void)hipFree(c.db);
+    (void)hipFree(c.dwino);
     c.dw = c.db = nullptr;
+    c.dwino = nullptr;
     bn_scale_shift(h, c.bn, c.cout, s, t);
     const auto& w = P(h, c.w + ".weight");
     const int taps = c.kt * c.kh * c.kw;
@@ -419,6 +439,14 @@ int clasfv_finalize(clasfv_t h) {
     int rc = upload_conv(
         c, [&](int o, int ci, int tap) { return w[((size_t)o * cin + ci) * taps + tap]; }, s, t, true);
     if (rc) return rc;
+    if (use_wino(c, bf16)) {
+      std::vector<double> wf((size_t)c.cout * cin * 9);
+      for (int o = 0; o < c.cout; ++o)
+        for (size_t i = 0; i < (size_t)cin * 9; ++i) wf[(size_t)o * cin * 9 + i] = (double)w[(size_t)o * cin * 9 + i] * s[o];
+      std::vector<float> u((size_t)16 * c.cin_p * c.cout_p);
+      wino_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, u.data());
+      if ((rc = upload(u, &c.dwino))) return rc;
+    }
   }
   // comb_1 + BN1 folded, split per tap (concat order stem, layer1, layer2, layer3, layer4)
   bn_scale_shift(h, "comb_batch_norm_1", 64, s, t);

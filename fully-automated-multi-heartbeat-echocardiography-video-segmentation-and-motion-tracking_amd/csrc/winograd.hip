@@ -1,0 +1,272 @@
+// Fused Winograd F(2x2, 3x3) convolution for the stride-1 1x3x3 spatial convs of R(2+1)D-18 (fp32).
+//
+// Reference op: the Conv2Plus1D spatial conv3d(kernel (1,3,3), stride 1, padding (0,1,1)) + BN(eval)
+// + ReLU of torchvision's r2plus1d_18 (called from src/model/R2plus1D_18_MotionNet.py:29-37). On
+// NVIDIA this is what cuDNN's Winograd algorithms compute; here it is one hand-written kernel.
+//
+//   Y(2x2 tile) = A^T [ sum_ci U_ci (.) V_ci ] A,   U = G g G^T (host, double),  V = B^T d B
+//
+// so 16 multiplies per 2x2 outputs and input channel instead of 36: the 16 transform elements
+// e = 4i + j become 16 independent GEMMs M_e[tile][co] = sum_ci V_e[tile][ci] U_e[ci][co], run on
+// exact-fp32 v_mfma_f32_16x16x4_f32.
+//
+// Block = 32 output tiles (2x2 pixels each, flattened over N,T,H/2,W/2) x 16*NT output channels,
+// 4 waves; wave w owns the transform row i = w (e = 4w..4w+3). Per chunk of 8 input channels:
+//  * raw 4x4 input patches (32 tiles x 16 pixels x 32 B = 16 KB) arrive by LDS-DMA
+//    (global_load_lds_dwordx4) into a 2-deep ring; pixel slot px of tile t is stored at
+//    px ^ (t & 7), which makes the transform's ds_read_b32 conflict-free;
+//  * all 256 threads transform one (tile, channel) patch each into V (16 KB, double-buffered,
+//    layout [e][tile][8 ci]) -- the next chunk's transform overlaps this chunk's MFMAs;
+//  * U_e for the wave's 4 e's comes straight from global memory (L2-resident, [chunk][e][co][8]),
+//    prefetched one chunk ahead into registers;
+//  * 2 K steps x 4 e x 2 m tiles x NT MFMAs per chunk and wave, one barrier per chunk.
+// Epilogue: per 16-channel slice, the accumulators go through LDS, every thread inverse-transforms
+// one (tile, channel) pair and applies bias, residual and ReLU to its 2x2 output pixels.
+#include "common.h"
+
+namespace {
+
+constexpr int BT = 32;                 // tiles per block
+constexpr int RAW_BYTES = BT * 16 * 32;  // 16 KB: [tile][px'][8 ci]
+constexpr int V_BYTES = 16 * BT * 32;    // 16 KB: [e][tile][8 ci]
+constexpr int RAW_STAGES = 3;            // raw ring depth: chunk k+3 is fetched while k+1 is transformed
+constexpr int M_STRIDE_T = 17;           // epilogue: floats per tile row of one e slice (16 co + pad)
+constexpr int M_STRIDE_E = BT * M_STRIDE_T + 4;
+
+__device__ inline int xcd_swizzle_w(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino(ConvParams p, int n_co,
+                                                                                             int n_tiles) {
+  __shared__ __align__(16) char smem[RAW_STAGES * RAW_BYTES + 2 * V_BYTES];
+  char* raw = smem;
+  char* vbuf = smem + RAW_STAGES * RAW_BYTES;
+
+  const float* x = reinterpret_cast<const float*>(p.x);
+  const float* U = reinterpret_cast<const float*>(p.w);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, l16 = lane & 15;
+  const int blk = xcd_swizzle_w(blockIdx.x, gridDim.x);
+  const int t0 = (blk / n_co) * BT, n0 = (blk % n_co) * 16 * NT;
+  const int H = p.Ho, W = p.Wo, C = p.Cin, CO = p.Cout;
+  const int TY = (H + 1) >> 1, TX = (W + 1) >> 1;
+  const int nchunk = C >> 3;
+
+  // ---- per-lane DMA sources: instruction j of this wave fills 16-B slot s = (wid + 4j)*64 + lane
+  int d_off[4];  // float offset of channel 0 of the source pixel, or -1 (zero padding)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int s = (wid + 4 * j) * 64 + lane;
+    const int tl = s >> 5, px = ((s & 31) >> 1) ^ (tl & 7), half = s & 1;
+    const int tg = t0 + tl;
+    int off = -1;
+    if (tg < n_tiles) {
+      const int f = tg / (TY * TX), r = tg - f * (TY * TX);
+      const int ty = r / TX, tx = r - ty * TX;
+      const int yy = 2 * ty - 1 + (px >> 2), xx = 2 * tx - 1 + (px & 3);
+      if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) off = ((f * H + yy) * W + xx) * C + half * 4;
+    }
+    d_off[j] = off;
+  }
+  auto issue_raw = [&](int chunk, int buf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const void* src = (d_off[j] >= 0 && chunk >= 0) ? (const void*)(x + (size_t)d_off[j] + chunk * 8) : p.zero;
+      char* dst = raw + buf * RAW_BYTES + (wid + 4 * j) * 1024;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  // ---- transform: thread = (tile tt, channel cc) of the chunk
+  const int tt = tid >> 3, cc = tid & 7;
+  auto transform = [&](int buf_raw, int buf_v) {
+    const float* rb = reinterpret_cast<const float*>(raw + buf_raw * RAW_BYTES) + tt * 128 + cc;
+    float d[16];
+#pragma unroll
+    for (int px = 0; px < 16; ++px) d[px] = rb[(px ^ (tt & 7)) * 8];
+    float t[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {  // B^T d
+      t[0 * 4 + c] = d[0 * 4 + c] - d[2 * 4 + c];
+      t[1 * 4 + c] = d[1 * 4 + c] + d[2 * 4 + c];
+      t[2 * 4 + c] = d[2 * 4 + c] - d[1 * 4 + c];
+      t[3 * 4 + c] = d[1 * 4 + c] - d[3 * 4 + c];
+    }
+    float* vb = reinterpret_cast<float*>(vbuf + buf_v * V_BYTES) + tt * 8 + cc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // (B^T d) B
+      vb[(4 * r + 0) * BT * 8] = t[4 * r + 0] - t[4 * r + 2];
+      vb[(4 * r + 1) * BT * 8] = t[4 * r + 1] + t[4 * r + 2];
+      vb[(4 * r + 2) * BT * 8] = t[4 * r + 2] - t[4 * r + 1];
+      vb[(4 * r + 3) * BT * 8] = t[4 * r + 1] - t[4 * r + 3];
+    }
+  };
+
+  // ---- U operands: lane (co = l16, q) of e-slot j, n tile nt: U[chunk][e][n0 + 16nt + l16][2q..2q+1]
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  const float* ub = U + ((size_t)(4 * wid) * CO + n0 + l16) * 8 + 2 * q;
+  f32x2 u0[4][NT], u1[4][NT], u2[4][NT];
+  auto load_u = [&](int chunk, f32x2 (&u)[4][NT]) {
+    const float* b = ub + (size_t)chunk * 16 * CO * 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) u[j][nt] = *reinterpret_cast<const f32x2*>(b + ((size_t)j * CO + nt * 16) * 8);
+  };
+  // Every fetch is issued unconditionally (past-the-end chunks re-read chunk 0 / the zero block into
+  // slots nobody reads again), so the number of memory operations per chunk is a constant and the
+  // waits below are exact: vmcnt(16) = "everything but the previous chunk's 4 DMAs + 12 U loads".
+  static_assert(4 + 4 * NT == 16, "wait counts assume NT = 3");
+  f32x4 acc[4][2][NT];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[j][m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- prologue: raw(0..2), U(0..1); transform(0)
+  issue_raw(0, 0);
+  load_u(0, u0);
+  issue_raw(nchunk > 1 ? 1 : -1, 1);
+  load_u(nchunk > 1 ? 1 : 0, u1);
+  issue_raw(nchunk > 2 ? 2 : -1, 2);
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (32 & 15) | ((32 >> 4) << 14));  // vmcnt(32): raw(0) landed
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  transform(0, 0);
+
+  const int a_off = l16 * 32 + q * 8;  // byte offset of the lane's V pair inside one (e, m tile)
+  // One chunk k: U(k) is in `uc`, U(k+2) is fetched into `un` (3-way rotation, no register copies);
+  // raw(k+3) is fetched into the ring slot raw(k) used; raw(k+1) is transformed into V[(k+1)&1]
+  // while the MFMAs consume V[k&1].
+  auto step = [&](int k, f32x2 (&uc)[4][NT], f32x2 (&un)[4][NT]) {
+    // raw(k+1) and U(k) were issued two chunks ago; only chunk k-1's 16 fetches may be in flight.
+    __builtin_amdgcn_s_waitcnt(0x0F70 | 16 & 15 | ((16 >> 4) << 14));  // vmcnt(16)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    issue_raw(k + 3 < nchunk ? k + 3 : -1, k % RAW_STAGES);
+    load_u(k + 2 < nchunk ? k + 2 : 0, un);
+    __builtin_amdgcn_sched_barrier(0);
+    if (k + 1 < nchunk) transform((k + 1) % RAW_STAGES, (k + 1) & 1);
+    const char* vb = vbuf + (k & 1) * V_BYTES + a_off;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x2 a[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+        a[m] = *reinterpret_cast<const f32x2*>(vb + (4 * wid + j) * (BT * 32) + m * 16 * 32);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s], uc[j][nt][s], acc[j][m][nt], 0, 0, 0);
+    }
+  };
+  // Full triples branch-free (keeps the compiler's own vmcnt bookkeeping exact), then the tail.
+  int k = 0;
+  for (; k + 3 <= nchunk; k += 3) {
+    step(k, u0, u2);
+    step(k + 1, u1, u0);
+    step(k + 2, u2, u1);
+  }
+  if (k < nchunk) step(k, u0, u2);
+  if (k + 1 < nchunk) step(k + 1, u1, u0);
+
+  // ---- epilogue: inverse transform per 16-channel slice through LDS
+  float* ms = reinterpret_cast<float*>(smem);
+  const int eco = tid & 15, etl = tid >> 4;  // thread's channel and first tile (second: +16)
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ms[(4 * wid + j) * M_STRIDE_E + (m * 16 + 4 * q + r) * M_STRIDE_T + l16] = acc[j][m][nt][r];
+    __syncthreads();
+    const int co = n0 + nt * 16 + eco;
+    const float bv = p.bias ? p.bias[co] : 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int tl = etl + 16 * h, tg = t0 + tl;
+      if (tg >= n_tiles) continue;
+      float mm[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) mm[e] = ms[e * M_STRIDE_E + tl * M_STRIDE_T + eco];
+      float rr[2][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {  // A^T M
+        rr[0][c] = mm[0 * 4 + c] + mm[1 * 4 + c] + mm[2 * 4 + c];
+        rr[1][c] = mm[1 * 4 + c] - mm[2 * 4 + c] - mm[3 * 4 + c];
+      }
+      const int f = tg / (TY * TX), rem = tg - f * (TY * TX);
+      const int ty = rem / TX, tx = rem - ty * TX;
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const float y0 = rr[a][0] + rr[a][1] + rr[a][2];
+        const float y1 = rr[a][1] - rr[a][2] - rr[a][3];
+        const int yy = 2 * ty + a;
+        if (yy >= H) continue;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int xx = 2 * tx + b;
+          if (xx >= W) continue;
+          const size_t o = ((size_t)(f * H + yy) * W + xx) * CO + co;
+          float v = (b ? y1 : y0) + bv;
+          if (p.res) v += reinterpret_cast<const float*>(p.res)[o];
+          if (p.relu) v = fmaxf(v, 0.f);
+          reinterpret_cast<float*>(p.y)[o] = v;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool wino_supported(const ConvParams& p) {
+  return !p.in_bf16 && !p.out_bf16 && !p.stem && !p.x2 && p.KT == 1 && p.KH == 3 && p.KW == 3 && p.sh == 1 &&
+         p.sw == 1 && p.st == 1 && p.ph == 1 && p.pw == 1 && p.pt == 0 && p.Cin % 16 == 0 && p.Cout % 48 == 0 &&
+         p.Ho == p.Hi && p.Wo == p.Wi && p.To == p.Ti &&
+         (size_t)p.N * p.To * p.Ho * p.Wo * (p.Cin > p.Cout ? p.Cin : p.Cout) < ((size_t)1 << 31);
+}
+
+// U: [Cin/8][16][Cout][8] transformed weights (wino_transform_weights).
+hipError_t launch_wino(const ConvParams& p, hipStream_t s) {
+  if (!wino_supported(p)) return hipErrorInvalidValue;
+  const int n_tiles = p.N * p.To * ((p.Ho + 1) / 2) * ((p.Wo + 1) / 2);
+  const int n_co = p.Cout / 48;
+  const int nb = (n_tiles + BT - 1) / BT;
+  hipLaunchKernelGGL((conv_wino<3>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles);
+  return hipGetLastError();
+}
+
+// Host: U[c/8][e][o][c%8] = (G g_{o,c} G^T)[e/4][e%4] in double, g = folded 3x3 kernel.
+void wino_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U) {
+  static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  for (size_t i = 0; i < (size_t)16 * cin_p * cout_p; ++i) U[i] = 0.f;
+  for (int o = 0; o < cout; ++o)
+    for (int c = 0; c < cin; ++c) {
+      const double* g = w + ((size_t)o * cin + c) * 9;
+      double tmp[4][3];
+      for (int i = 0; i < 4; ++i)
+        for (int v = 0; v < 3; ++v) tmp[i][v] = G[i][0] * g[0 * 3 + v] + G[i][1] * g[1 * 3 + v] + G[i][2] * g[2 * 3 + v];
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+          const double u = tmp[i][0] * G[j][0] + tmp[i][1] * G[j][1] + tmp[i][2] * G[j][2];
+          U[(((size_t)(c / 8) * 16 + 4 * i + j) * cout_p + o) * 8 + (c % 8)] = (float)u;
+        }
+    }
+}

@@ -322,3 +322,25 @@ def test_forward_bf16_vs_reference_golden_config4_tolerance(model):
     s32, _ = m16(torch.from_numpy(np.ascontiguousarray(v[None, :, s:s + 32])))
     s_ref, _ = model(torch.from_numpy(np.ascontiguousarray(v[None, :, s:s + 32])))
     assert torch.equal(s32, s_ref)
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 32, 112, 112), (2, 3, 16, 64, 48)])
+def test_winograd_path_matches_direct_conv(model, monkeypatch, shape):
+    """The fused Winograd F(2x2,3x3) kernel (default for stride-1 1x3x3 fp32 convs) against the
+    direct implicit-GEMM kernel (CLASFV_WINOGRAD=0), and both against the CPU oracle."""
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    rng = np.random.default_rng(17)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32))
+    s_w, m_w = model(x)
+    monkeypatch.setenv("CLASFV_WINOGRAD", "0")
+    direct = R2plus1D_18_MotionNet(pretrained=False)
+    s_d, m_d = direct(x)
+    monkeypatch.delenv("CLASFV_WINOGRAD")
+    assert not torch.equal(s_w, s_d)  # two different kernels really ran
+    np.testing.assert_allclose(s_w.cpu().numpy(), s_d.cpu().numpy(), rtol=0, atol=2e-3)
+    np.testing.assert_allclose(m_w.cpu().numpy(), m_d.cpu().numpy(), rtol=0, atol=1e-5)
+    if shape[2] <= 16:
+        from oracle import r2plus1d_ref as R
+        import clasfv_amd.weights as W
+        rs, rm = R.forward(W.synthetic_state_dict(W.DEFAULT_SEED), x.numpy())
+        np.testing.assert_allclose(s_w.cpu().numpy(), rs.numpy(), rtol=0, atol=3e-3)

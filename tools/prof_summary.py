@@ -28,7 +28,7 @@ def forwards(seq, name_of=lambda r: r[0]):
     out, cur = [], []
     for r in seq:
         n = name_of(r)
-        if n.startswith("conv_") or n.startswith("pack_input"):
+        if "conv_" in n or n.startswith("pack_input"):
             cur.append(r)
         elif n.startswith("decoder_kernel"):
             cur.append(r)
@@ -64,7 +64,7 @@ def main():
             if fws:
                 kb = sum(v for _, v in fws[-1])
                 print(f"\n{cn} last forward: {kb / 1024:.1f} MiB raw, x{corr:g} corrected = {kb * corr / 1024:.1f} MiB")
-                conv_kb = sum(v for n, v in fws[-1] if n.startswith("conv"))
+                conv_kb = sum(v for n, v in fws[-1] if "conv_" in n)
                 dec_kb = sum(v for n, v in fws[-1] if n.startswith("decoder"))
                 print(f"  conv_igemm {conv_kb * corr / 1024:.1f} MiB, decoder {dec_kb * corr / 1024:.1f} MiB")
 
