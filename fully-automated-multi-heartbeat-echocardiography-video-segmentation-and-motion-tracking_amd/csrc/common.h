@@ -52,7 +52,7 @@ void conv_pick_tile(int M, int cout_p, int force_nt, int* mt, int* bn);
 // Fused Winograd F(2x2,3x3) path for stride-1 1x3x3 fp32 convs; p.w = transformed weights.
 bool wino_supported(const ConvParams& p);
 hipError_t launch_wino(const ConvParams& p, hipStream_t s);
-// U[cin_p/8][16][cout_p][8] from folded weights w[cout][cin][3][3] (double).
+// U[cin_p/8][4][cout_p][4][4][2] from folded weights w[cout][cin][3][3] (double).
 void wino_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 hipError_t launch_decoder(const DecParams& p, hipStream_t s);
 hipError_t launch_pack_input(const float* x, float* y, int N, int T, int HW, hipStream_t s);

@@ -17,21 +17,21 @@
 //    px ^ (t & 7), which makes the transform's ds_read_b32 conflict-free;
 //  * all 256 threads transform one (tile, channel) patch each into V (16 KB, double-buffered,
 //    layout [e][tile][8 ci]) -- the next chunk's transform overlaps this chunk's MFMAs;
-//  * U_e for the wave's 4 e's comes straight from global memory (L2-resident, [chunk][e][co][8]),
-//    prefetched one chunk ahead into registers;
+//  * U_e for the wave's 4 e's comes straight from global memory (16-B loads, [chunk][i][co][8 ci][j]),
+//    prefetched two chunks ahead into registers;
 //  * 2 K steps x 4 e x 2 m tiles x NT MFMAs per chunk and wave, one barrier per chunk.
-// Epilogue: per 16-channel slice, the accumulators go through LDS, every thread inverse-transforms
-// one (tile, channel) pair and applies bias, residual and ReLU to its 2x2 output pixels.
+// Epilogue: each wave applies the column half of the inverse transform to its row of M in registers,
+// the row half goes through LDS (one barrier), then bias, residual and ReLU on the 2x2 output pixels.
 #include "common.h"
 
 namespace {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int BT = 32;                 // tiles per block
 constexpr int RAW_BYTES = BT * 16 * 32;  // 16 KB: [tile][px'][8 ci]
 constexpr int V_BYTES = 16 * BT * 32;    // 16 KB: [e][tile][8 ci]
 constexpr int RAW_STAGES = 3;            // raw ring depth: chunk k+3 is fetched while k+1 is transformed
-constexpr int M_STRIDE_T = 17;           // epilogue: floats per tile row of one e slice (16 co + pad)
-constexpr int M_STRIDE_E = BT * M_STRIDE_T + 4;
 
 __device__ inline int xcd_swizzle_w(int b, int nb) {
   const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
@@ -97,7 +97,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       t[2 * 4 + c] = d[2 * 4 + c] - d[1 * 4 + c];
       t[3 * 4 + c] = d[1 * 4 + c] - d[3 * 4 + c];
     }
-    float* vb = reinterpret_cast<float*>(vbuf + buf_v * V_BYTES) + tt * 8 + cc;
+    // V[e][tile & 15][ci >> 1][tile >> 4][ci & 1]: one lane's A operands of both m tiles and both
+    // K steps are 16 contiguous bytes (a conflict-free ds_read_b128)
+    float* vb = reinterpret_cast<float*>(vbuf + buf_v * V_BYTES) + (((tt & 15) * 4 + (cc >> 1)) * 2 + (tt >> 4)) * 2 +
+                (cc & 1);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {  // (B^T d) B
       vb[(4 * r + 0) * BT * 8] = t[4 * r + 0] - t[4 * r + 2];
@@ -107,21 +110,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
   };
 
-  // ---- U operands: lane (co = l16, q) of e-slot j, n tile nt: U[chunk][e][n0 + 16nt + l16][2q..2q+1]
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  const float* ub = U + ((size_t)(4 * wid) * CO + n0 + l16) * 8 + 2 * q;
-  f32x2 u0[4][NT], u1[4][NT], u2[4][NT];
-  auto load_u = [&](int chunk, f32x2 (&u)[4][NT]) {
-    const float* b = ub + (size_t)chunk * 16 * CO * 8;
+  // ---- U operands: lane (co = l16, q) of wave (e row) i, n tile nt reads the 8 floats
+  // U[chunk][i][co][q][j][s] (e = 4i + j, ci = 8 chunk + 2q + s) as two 16-B loads.
+  const float* ub = U + (((size_t)wid * CO + n0 + l16) * 4 + q) * 8;
+  f32x4 u0[NT][2], u1[NT][2], u2[NT][2];
+  auto load_u = [&](int chunk, f32x4 (&u)[NT][2]) {
+    const float* b = ub + (size_t)chunk * 4 * CO * 32;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) u[j][nt] = *reinterpret_cast<const f32x2*>(b + ((size_t)j * CO + nt * 16) * 8);
+      for (int h = 0; h < 2; ++h) u[nt][h] = *reinterpret_cast<const f32x4*>(b + (size_t)nt * 16 * 32 + h * 4);
   };
   // Every fetch is issued unconditionally (past-the-end chunks re-read chunk 0 / the zero block into
   // slots nobody reads again), so the number of memory operations per chunk is a constant and the
   // waits below are exact: vmcnt(16) = "everything but the previous chunk's 4 DMAs + 12 U loads".
-  static_assert(4 + 4 * NT == 16, "wait counts assume NT = 3");
+  static_assert(4 + 2 * NT == 10, "wait counts assume NT = 3");
   f32x4 acc[4][2][NT];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -137,18 +140,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   load_u(nchunk > 1 ? 1 : 0, u1);
   issue_raw(nchunk > 2 ? 2 : -1, 2);
   __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_waitcnt(0x0F70 | (32 & 15) | ((32 >> 4) << 14));  // vmcnt(32): raw(0) landed
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (20 & 15) | ((20 >> 4) << 14));  // vmcnt(20): raw(0) landed
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   transform(0, 0);
 
-  const int a_off = l16 * 32 + q * 8;  // byte offset of the lane's V pair inside one (e, m tile)
+  const int a_off = (l16 * 4 + q) * 16;  // byte offset of the lane's 4 V values inside one e slice
   // One chunk k: U(k) is in `uc`, U(k+2) is fetched into `un` (3-way rotation, no register copies);
   // raw(k+3) is fetched into the ring slot raw(k) used; raw(k+1) is transformed into V[(k+1)&1]
   // while the MFMAs consume V[k&1].
-  auto step = [&](int k, f32x2 (&uc)[4][NT], f32x2 (&un)[4][NT]) {
-    // raw(k+1) and U(k) were issued two chunks ago; only chunk k-1's 16 fetches may be in flight.
-    __builtin_amdgcn_s_waitcnt(0x0F70 | 16 & 15 | ((16 >> 4) << 14));  // vmcnt(16)
+  auto step = [&](int k, f32x4 (&uc)[NT][2], f32x4 (&un)[NT][2]) {
+    // raw(k+1) and U(k) were issued two chunks ago; only chunk k-1's 10 fetches may be in flight.
+    __builtin_amdgcn_s_waitcnt(0x0F70 | 10);  // vmcnt(10)
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -159,17 +162,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const char* vb = vbuf + (k & 1) * V_BYTES + a_off;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      f32x2 a[2];
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-        a[m] = *reinterpret_cast<const f32x2*>(vb + (4 * wid + j) * (BT * 32) + m * 16 * 32);
+      const f32x4 a = *reinterpret_cast<const f32x4*>(vb + (4 * wid + j) * (BT * 32));  // {m0 s0, m0 s1, m1 s0, m1 s1}
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt)
-            acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s], uc[j][nt][s], acc[j][m][nt], 0, 0, 0);
+            acc[j][m][nt] =
+                __builtin_amdgcn_mfma_f32_16x16x4f32(a[2 * m + s], uc[nt][j >> 1][(j & 1) * 2 + s], acc[j][m][nt], 0, 0, 0);
     }
   };
   // Full triples branch-free (keeps the compiler's own vmcnt bookkeeping exact), then the tail.
@@ -182,53 +183,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (k < nchunk) step(k, u0, u2);
   if (k + 1 < nchunk) step(k + 1, u1, u0);
 
-  // ---- epilogue: inverse transform per 16-channel slice through LDS
-  float* ms = reinterpret_cast<float*>(smem);
-  const int eco = tid & 15, etl = tid >> 4;  // thread's channel and first tile (second: +16)
+  // ---- epilogue: Y = A^T M A. Wave i holds row i of M: the column combination (. A) is done in
+  // registers, Z_i = (M_i0 + M_i1 + M_i2, M_i1 - M_i2 - M_i3); the row combination (A^T .) needs all
+  // four waves and goes through LDS: Z[i][tile][co][2] (48 KB), one barrier.
+  f32x2* zs = reinterpret_cast<f32x2*>(smem);
+  __syncthreads();  // everyone is done with raw / V
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    __syncthreads();
+  for (int m = 0; m < 2; ++m)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          ms[(4 * wid + j) * M_STRIDE_E + (m * 16 + 4 * q + r) * M_STRIDE_T + l16] = acc[j][m][nt][r];
-    __syncthreads();
-    const int co = n0 + nt * 16 + eco;
-    const float bv = p.bias ? p.bias[co] : 0.f;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int tl = etl + 16 * h, tg = t0 + tl;
-      if (tg >= n_tiles) continue;
-      float mm[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) mm[e] = ms[e * M_STRIDE_E + tl * M_STRIDE_T + eco];
-      float rr[2][4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {  // A^T M
-        rr[0][c] = mm[0 * 4 + c] + mm[1 * 4 + c] + mm[2 * 4 + c];
-        rr[1][c] = mm[1 * 4 + c] - mm[2 * 4 + c] - mm[3 * 4 + c];
+      for (int r = 0; r < 4; ++r) {
+        const float m0 = acc[0][m][nt][r], m1 = acc[1][m][nt][r], m2 = acc[2][m][nt][r], m3 = acc[3][m][nt][r];
+        zs[(wid * BT + m * 16 + 4 * q + r) * (16 * NT) + nt * 16 + l16] = f32x2{m0 + m1 + m2, m1 - m2 - m3};
       }
-      const int f = tg / (TY * TX), rem = tg - f * (TY * TX);
-      const int ty = rem / TX, tx = rem - ty * TX;
+  __syncthreads();
+  constexpr int PAIRS = BT * 16 * NT;  // (tile, channel) pairs of the block
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const float y0 = rr[a][0] + rr[a][1] + rr[a][2];
-        const float y1 = rr[a][1] - rr[a][2] - rr[a][3];
-        const int yy = 2 * ty + a;
-        if (yy >= H) continue;
+  for (int k2 = 0; k2 < PAIRS / 256; ++k2) {
+    const int pr = tid + 256 * k2;
+    const int tl = pr / (16 * NT), cl = pr - tl * (16 * NT);
+    const int tg = t0 + tl;
+    if (tg >= n_tiles) continue;
+    f32x2 z[4];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int xx = 2 * tx + b;
-          if (xx >= W) continue;
-          const size_t o = ((size_t)(f * H + yy) * W + xx) * CO + co;
-          float v = (b ? y1 : y0) + bv;
-          if (p.res) v += reinterpret_cast<const float*>(p.res)[o];
-          if (p.relu) v = fmaxf(v, 0.f);
-          reinterpret_cast<float*>(p.y)[o] = v;
-        }
+    for (int i = 0; i < 4; ++i) z[i] = zs[(i * BT + tl) * (16 * NT) + cl];
+    const int co = n0 + cl;
+    const float bv = p.bias ? p.bias[co] : 0.f;
+    const int f = tg / (TY * TX), rem = tg - f * (TY * TX);
+    const int ty = rem / TX, tx = rem - ty * TX;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int yy = 2 * ty + a;
+      if (yy >= H) continue;
+      const f32x2 y = a == 0 ? z[0] + z[1] + z[2] : z[1] - z[2] - z[3];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int xx = 2 * tx + b;
+        if (xx >= W) continue;
+        const size_t o = ((size_t)(f * H + yy) * W + xx) * CO + co;
+        float v = y[b] + bv;
+        if (p.res) v += reinterpret_cast<const float*>(p.res)[o];
+        if (p.relu) v = fmaxf(v, 0.f);
+        reinterpret_cast<float*>(p.y)[o] = v;
       }
     }
   }
@@ -243,7 +240,7 @@ bool wino_supported(const ConvParams& p) {
          (size_t)p.N * p.To * p.Ho * p.Wo * (p.Cin > p.Cout ? p.Cin : p.Cout) < ((size_t)1 << 31);
 }
 
-// U: [Cin/8][16][Cout][8] transformed weights (wino_transform_weights).
+// U: [Cin/8][4][Cout][4][4][2] transformed weights (wino_transform_weights).
 hipError_t launch_wino(const ConvParams& p, hipStream_t s) {
   if (!wino_supported(p)) return hipErrorInvalidValue;
   const int n_tiles = p.N * p.To * ((p.Ho + 1) / 2) * ((p.Wo + 1) / 2);
@@ -253,7 +250,7 @@ hipError_t launch_wino(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Host: U[c/8][e][o][c%8] = (G g_{o,c} G^T)[e/4][e%4] in double, g = folded 3x3 kernel.
+// Host: U[c/8][i][o][(c%8)/2][j][c%2] = (G g_{o,c} G^T)[i][j] in double, g = folded 3x3 kernel.
 void wino_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U) {
   static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
   for (size_t i = 0; i < (size_t)16 * cin_p * cout_p; ++i) U[i] = 0.f;
@@ -266,7 +263,7 @@ void wino_transform_weights(const double* w, int cout, int cin, int cout_p, int 
       for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) {
           const double u = tmp[i][0] * G[j][0] + tmp[i][1] * G[j][1] + tmp[i][2] * G[j][2];
-          U[(((size_t)(c / 8) * 16 + 4 * i + j) * cout_p + o) * 8 + (c % 8)] = (float)u;
+          U[((((size_t)(c / 8) * 4 + i) * cout_p + o) * 4 + (c % 8) / 2) * 8 + j * 2 + (c % 2)] = (float)u;
         }
     }
 }

@@ -2,9 +2,21 @@
 usage: python tools/pmc_summary.py OUTDIR"""
 import glob
 import os
+import re
 import sqlite3
 import sys
 from collections import defaultdict
+
+
+def short(name):
+    """Readable kernel name: the identifier inside an anonymous-namespace mangled name."""
+    m = re.match(r"_ZN12_GLOBAL__N_1(\d+)", name)
+    if m:
+        n = int(m.group(1))
+        base = name[m.end():m.end() + n]
+        t = re.search(r"I(DF16b|f)L", name)
+        return base + ("_bf16" if t and t.group(1) == "DF16b" else "")
+    return name
 
 
 def load(db):
@@ -15,7 +27,7 @@ def load(db):
     names = {}
     for d, k, cn, v, g, w in rows:
         per[d][cn] = per[d].get(cn, 0) + v
-        names[d] = (k, g // max(w, 1))
+        names[d] = (short(k), g // max(w, 1))
     return per, names
 
 
@@ -35,7 +47,8 @@ def main():
                 merged[key][cn] += v
     cols = ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU",
             "SQ_ACTIVE_INST_LDS", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
-            "GRBM_GUI_ACTIVE", "TCC_HIT_sum", "TCC_MISS_sum", "SQ_INSTS_MFMA", "SQ_INSTS_VALU"]
+            "GRBM_GUI_ACTIVE", "TCC_HIT_sum", "TCC_MISS_sum", "SQ_INSTS_MFMA", "SQ_INSTS_VALU", "TA_BUSY_avr",
+            "TA_FLAT_READ_WAVEFRONTS_sum", "TA_ADDR_STALLED_BY_TC_CYCLES_sum", "TA_DATA_STALLED_BY_TC_CYCLES_sum"]
     print("idx kernel            grid   " + " ".join(f"{c[3:15]:>12s}" for c in cols))
     for key in sorted(merged):
         m = merged[key]
@@ -49,7 +62,8 @@ def main():
               f"valu {m.get('SQ_ACTIVE_INST_VALU', 0) / wave:5.2f} lds {m.get('SQ_ACTIVE_INST_LDS', 0) / wave:5.2f} "
               f"bank_conf/lds_active {m.get('SQ_LDS_BANK_CONFLICT', 0) / max(m.get('SQ_LDS_IDX_ACTIVE', 1), 1):5.2f} "
               f"mfma_busy/gui {m.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / max(m.get('GRBM_GUI_ACTIVE', 1), 1):8.2f} "
-              f"L2hit {m.get('TCC_HIT_sum', 0) / max(m.get('TCC_HIT_sum', 0) + m.get('TCC_MISS_sum', 0), 1):5.2f}")
+              f"L2hit {m.get('TCC_HIT_sum', 0) / max(m.get('TCC_HIT_sum', 0) + m.get('TCC_MISS_sum', 0), 1):5.2f} "
+              f"ta_busy/gui {m.get('TA_BUSY_avr', 0) / max(m.get('GRBM_GUI_ACTIVE', 1), 1):5.2f}")
 
 
 if __name__ == "__main__":
