@@ -54,5 +54,10 @@ bool wino_supported(const ConvParams& p);
 hipError_t launch_wino(const ConvParams& p, hipStream_t s);
 // U[cin_p/8][4][cout_p][4][4][2] from folded weights w[cout][cin][3][3] (double).
 void wino_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
+// Fused Winograd F(4,3)-in-time path for stride-1 3x1x1 fp32 convs; p.w = transformed weights.
+bool winot_supported(const ConvParams& p);
+hipError_t launch_winot(const ConvParams& p, hipStream_t s);
+// U[cin_p/8][6][cout_p/64][64][8] from folded weights w[cout][cin][3] (double).
+void winot_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 hipError_t launch_decoder(const DecParams& p, hipStream_t s);
 hipError_t launch_pack_input(const float* x, float* y, int N, int T, int HW, hipStream_t s);

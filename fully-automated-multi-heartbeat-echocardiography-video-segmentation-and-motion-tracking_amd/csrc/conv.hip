@@ -51,17 +51,25 @@ __device__ inline void epilogue(const ConvParams& p, const f32x4 (&acc)[MT][NT],
     const int n = n0 + j * 16 + l16;
     if (n >= p.Cout) continue;
     const float bv = p.bias ? p.bias[n] : 0.f;
+    // the residual values of this column are all loaded before any store (res may alias y, so a
+    // load after a store would have to wait for it)
+    float rv[MT][4];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m_base + i * 16 + q * 4 + r;
+        rv[i][r] = (p.res && m < p.M) ? load_res(p.res, (size_t)m * p.Cout + n, p.out_bf16) : 0.f;
+      }
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m_base + i * 16 + q * 4 + r;
         if (m >= p.M) continue;
-        float v = acc[i][j][r] + bv;
-        const size_t o = (size_t)m * p.Cout + n;
-        if (p.res) v += load_res(p.res, o, p.out_bf16);
+        float v = acc[i][j][r] + bv + rv[i][r];
         if (p.relu) v = fmaxf(v, 0.f);
-        store_out(p.y, o, v, p.out_bf16);
+        store_out(p.y, (size_t)m * p.Cout + n, v, p.out_bf16);
       }
     }
   }

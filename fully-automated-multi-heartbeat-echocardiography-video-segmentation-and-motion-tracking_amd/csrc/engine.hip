@@ -78,9 +78,18 @@ struct Conv {
   void* dw = nullptr;     // weights, dtype of the conv's input
   float* db = nullptr;    // folded-BN bias (fp32)
   float* dwino = nullptr;  // Winograd F(2x2,3x3) transformed weights (fp32 stride-1 1x3x3 convs)
+  float* dwinot = nullptr;  // Winograd F(4,3)-in-time transformed weights (fp32 stride-1 3x1x1 convs)
 };
 
 // fp32 stride-1 1x3x3 convs run on the fused Winograd kernel unless CLASFV_WINOGRAD=0.
+// fp32 stride-1 3x1x1 convs run on the fused temporal Winograd kernel unless CLASFV_WINOGRAD=0.
+bool use_winot(const Conv& c, bool bf16) {
+  const char* e = getenv("CLASFV_WINOGRAD");
+  if (e && e[0] == '0') return false;
+  return !bf16 && (c.role == STEM_T || c.role == TP1 || c.role == TP2) && c.kt == 3 && c.kh == 1 && c.kw == 1 &&
+         c.st == 1 && c.cin_p % 8 == 0 && c.cout_p % 64 == 0;
+}
+
 bool use_wino(const Conv& c, bool bf16) {
   const char* e = getenv("CLASFV_WINOGRAD");
   if (e && e[0] == '0') return false;
@@ -294,6 +303,14 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
     }
     p.w = c.dw;
   }
+  if (c.dwinot) {
+    p.w = c.dwinot;
+    if (winot_supported(p)) {
+      HIP_TRY(launch_winot(p, s));
+      return CLASFV_OK;
+    }
+    p.w = c.dw;
+  }
   int mt = 2, bn = c.cout_p;  // stem: one N tile (48 fp32 / 64 bf16 channels)
   if (!c.stem) {
     static const int force_nt = getenv("CLASFV_CONV_NT") ? atoi(getenv("CLASFV_CONV_NT")) : 0;
@@ -371,6 +388,7 @@ int clasfv_destroy(clasfv_t h) {
     (void)hipFree(c.dw);
     (void)hipFree(c.db);
     (void)hipFree(c.dwino);
+    (void)hipFree(c.dwinot);
   }
   for (auto& c : h->proj) (void)hipFree(c.dw);
   (void)hipFree(h->b1);
@@ -430,8 +448,9 @@ int clasfv_finalize(clasfv_t h) {
     (void)hipFree(c.dw);
     (void)hipFree(c.db);
     (void)hipFree(c.dwino);
+    (void)hipFree(c.dwinot);
     c.dw = c.db = nullptr;
-    c.dwino = nullptr;
+    c.dwino = c.dwinot = nullptr;
     bn_scale_shift(h, c.bn, c.cout, s, t);
     const auto& w = P(h, c.w + ".weight");
     const int taps = c.kt * c.kh * c.kw;
@@ -446,6 +465,14 @@ int clasfv_finalize(clasfv_t h) {
       std::vector<float> u((size_t)16 * c.cin_p * c.cout_p);
       wino_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, u.data());
       if ((rc = upload(u, &c.dwino))) return rc;
+    }
+    if (use_winot(c, bf16)) {
+      std::vector<double> wf((size_t)c.cout * cin * 3);
+      for (int o = 0; o < c.cout; ++o)
+        for (size_t i = 0; i < (size_t)cin * 3; ++i) wf[(size_t)o * cin * 3 + i] = (double)w[(size_t)o * cin * 3 + i] * s[o];
+      std::vector<float> u((size_t)6 * c.cin_p * c.cout_p);
+      winot_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, u.data());
+      if ((rc = upload(u, &c.dwinot))) return rc;
     }
   }
   // comb_1 + BN1 folded, split per tap (concat order stem, layer1, layer2, layer3, layer4)

@@ -1,0 +1,270 @@
+// Fused 1-D Winograd F(4,3) along time for the stride-1 3x1x1 temporal convs of R(2+1)D-18 (fp32).
+//
+// Reference op: the Conv2Plus1D temporal conv3d(kernel (3,1,1), stride 1, padding (1,0,0)) + BN(eval)
+// (+ residual) + ReLU of torchvision's r2plus1d_18, and the stem's second conv (called from
+// src/model/R2plus1D_18_MotionNet.py:29-37).
+//
+//   y[4 frames] = A^T [ sum_ci U_ci (.) V_ci ],   U = G g (host, double, 6 values per 3 taps),
+//                                                V = B^T d (6 input frames)
+//
+// 6 multiplies per 4 outputs and input channel instead of 12: the 6 transform elements are 6
+// independent GEMMs M_e[tile][co] = sum_ci V_e[tile][ci] U_e[ci][co] on exact-fp32
+// v_mfma_f32_16x16x4_f32. Interpolation points 0, +-1, +-2, inf.
+//
+// Block = 6 waves (wave e owns transform element e) x 64 tiles (4 frames at one pixel) x 64 output
+// channels; 2 blocks per CU. Per chunk of 8 input channels:
+//  * raw input (64 tiles x 6 frames x 32 B = 12 KB, [frame][tile][8 ci]) and U (6 e x 64 co x 32 B
+//    = 12 KB, [e][co][8 ci]) arrive by LDS-DMA into 2-deep rings (wave e fetches its own U_e);
+//  * all threads transform (tile, channel) columns into V (12 KB, [e][tile][8 ci], double-buffered);
+//    the transform of chunk k+1 overlaps the MFMAs of chunk k; one barrier per chunk;
+//  * 2 K steps x 4 m tiles x 4 n tiles = 32 MFMAs per chunk and wave.
+// Epilogue: two 32-channel passes through LDS; each thread applies A^T to one (tile, channel) pair
+// and writes 4 frames with bias, residual and ReLU.
+#include "common.h"
+
+namespace {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int BT = 64;                   // tiles per block
+constexpr int BN = 64;                   // output channels per block
+constexpr int NTHR = 384;                // 6 waves
+constexpr int RAW_BYTES = 6 * BT * 32;   // 12 KB
+constexpr int V_BYTES = 6 * BT * 32;     // 12 KB
+constexpr int U_BYTES = 6 * BN * 32;     // 12 KB
+constexpr int LDS_BYTES = 2 * (RAW_BYTES + V_BYTES + U_BYTES);  // 72 KB
+constexpr int MS = 33;                   // epilogue: floats per tile row (32 channels + pad)
+
+__device__ inline int xcd_swizzle_t(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_winot(ConvParams p, int n_co,
+                                                                                              int n_tiles) {
+  extern __shared__ __align__(16) char smem[];
+  char* raw = smem;
+  char* vbuf = smem + 2 * RAW_BYTES;
+  char* ubuf = vbuf + 2 * V_BYTES;
+
+  const float* x = reinterpret_cast<const float*>(p.x);
+  const float* U = reinterpret_cast<const float*>(p.w);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // = transform element e
+  const int q = lane >> 4, l16 = lane & 15;
+  const int blk = xcd_swizzle_t(blockIdx.x, gridDim.x);
+  const int tb = blk / n_co, cb = blk - tb * n_co;
+  const int t0 = tb * BT;
+  const int T = p.To, HW = p.Ho * p.Wo, C = p.Cin, CO = p.Cout;
+  const int TT = T >> 2;
+  const int nchunk = C >> 3;
+
+  // ---- raw DMA: 12 instructions per chunk, 2 per wave; slot s = I*64 + lane -> (frame, tile, half)
+  int d_off[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int s = (wid * 2 + j) * 64 + lane;
+    const int f = s >> 7, rem = s & 127, tl = rem >> 1, half = rem & 1;
+    const int tg = t0 + tl;
+    int off = -1;
+    if (tg < n_tiles) {
+      const int nt_ = tg / HW, pix = tg - nt_ * HW;
+      const int n = nt_ / TT, tau = nt_ - n * TT;
+      const int t = 4 * tau - 1 + f;
+      if ((unsigned)t < (unsigned)T) off = ((n * T + t) * HW + pix) * C + half * 4;
+    }
+    d_off[j] = off;
+  }
+  // Past-the-end chunks fetch the zero block (or chunk 0 of U) into a free slot: every chunk issues
+  // exactly 2 raw + 2 U DMAs per wave, so the counted waits below are exact.
+  auto issue_raw = [&](int k, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const void* src = (k < nchunk && d_off[j] >= 0) ? (const void*)(x + (size_t)d_off[j] + k * 8) : p.zero;
+      char* dst = raw + buf * RAW_BYTES + (wid * 2 + j) * 1024;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+  // U_e for chunk k: 2 KB at U + ((k*6 + e)*n_co + cb)*512 floats
+  const float* ub = U + ((size_t)wid * n_co + cb) * 512 + lane * 4;
+  auto issue_u = [&](int k, int buf) __attribute__((always_inline)) {
+    const int kk = k < nchunk ? k : 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const void* src = (const void*)(ub + (size_t)kk * 6 * n_co * 512 + j * 256);
+      char* dst = ubuf + buf * U_BYTES + wid * 2048 + j * 1024;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  // ---- transform: (tile, channel) columns p = tid, tid + 384 (< 512)
+  auto transform = [&](int buf) __attribute__((always_inline)) {
+    const float* rb = reinterpret_cast<const float*>(raw + buf * RAW_BYTES);
+    float* vb = reinterpret_cast<float*>(vbuf + buf * V_BYTES);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pr = tid + NTHR * h;
+      if (pr < BT * 8) {
+        float d[6];
+#pragma unroll
+        for (int f = 0; f < 6; ++f) d[f] = rb[f * (BT * 8) + pr];
+        const float e1 = d[3] + d[4], e2 = d[1] + d[2], e3 = d[4] - d[3], e4 = d[1] - d[2];
+        float* o = vb + pr;
+        o[0 * BT * 8] = 4.f * d[0] - 5.f * d[2] + d[4];
+        o[1 * BT * 8] = e1 - 4.f * e2;
+        o[2 * BT * 8] = e3 + 4.f * e4;
+        o[3 * BT * 8] = (d[4] - d[2]) + 2.f * (d[3] - d[1]);
+        o[4 * BT * 8] = (d[4] - d[2]) - 2.f * (d[3] - d[1]);
+        o[5 * BT * 8] = 4.f * d[1] - 5.f * d[3] + d[5];
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Chunk k: raw(k+2) is fetched at its start, U(k+2) at its end (the U slot is read until then);
+  // at the top of chunk k, raw(k+1) and U(k) must have landed: only U(k+1)'s 2 DMAs are newer.
+  issue_raw(0, 0);
+  issue_u(0, 0);
+  issue_raw(1, 1);
+  issue_u(1, 1);
+  __builtin_amdgcn_s_waitcnt(0x0F70 | 6);  // vmcnt(6): raw(0) landed
+  __builtin_amdgcn_s_barrier();
+  transform(0);
+
+  const int a_off = (l16 * 8 + 2 * q) * 4;  // byte offset of the lane's (tile l16, ci 2q..2q+1) pair
+  for (int k = 0; k < nchunk; ++k) {
+    __builtin_amdgcn_s_waitcnt(0x0F70 | 2);  // vmcnt(2)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // also: V(k) complete, everyone done with V(k-1) and raw(k)
+    __builtin_amdgcn_sched_barrier(0);
+    issue_raw(k + 2, k & 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (k + 1 < nchunk) transform((k + 1) & 1);
+    const char* vb = vbuf + (k & 1) * V_BYTES + wid * (BT * 32) + a_off;
+    const char* bb = ubuf + (k & 1) * U_BYTES + wid * 2048 + a_off;
+    f32x2 a[4], b[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) a[m] = *reinterpret_cast<const f32x2*>(vb + m * 16 * 32);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) b[n] = *reinterpret_cast<const f32x2*>(bb + n * 16 * 32);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m][s], b[n][s], acc[m][n], 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of its U(k) slot are done
+    __builtin_amdgcn_sched_barrier(0);
+    issue_u(k + 2, k & 1);  // the U slot is private to the wave (its own e)
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // drain the past-the-end DMAs before LDS is reused
+
+  // ---- epilogue: y[4 frames] = A^T M, two passes of 32 channels. Each thread's residual values
+  // are fetched before the LDS exchange (all loads ahead of all stores: no load waits on a store).
+  float* ms = reinterpret_cast<float*>(smem);
+  constexpr int IT = (BT * 32 + NTHR - 1) / NTHR;  // (tile, channel) pairs per thread and pass
+  const float* res = reinterpret_cast<const float*>(p.res);
+  float* yout = reinterpret_cast<float*>(p.y);
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    size_t o0[IT];
+    bool ok[IT];
+    float rv[IT][4];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int pr = tid + NTHR * it;
+      const int tl = pr >> 5, cl = pr & 31;
+      const int tg = t0 + tl;
+      ok[it] = pr < BT * 32 && tg < n_tiles;
+      const int tgc = ok[it] ? tg : 0;
+      const int nt_ = tgc / HW, pix = tgc - nt_ * HW;
+      const int n = nt_ / TT, tau = nt_ - n * TT;
+      o0[it] = ((size_t)(n * T + 4 * tau) * HW + pix) * CO + cb * BN + pass * 32 + cl;
+#pragma unroll
+      for (int a2 = 0; a2 < 4; ++a2) rv[it][a2] = (res && ok[it]) ? res[o0[it] + (size_t)a2 * HW * CO] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ms[(wid * BT + m * 16 + 4 * q + r) * MS + n2 * 16 + l16] = acc[m][2 * pass + n2][r];
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      if (!ok[it]) continue;
+      const int pr = tid + NTHR * it;
+      const int tl = pr >> 5, cl = pr & 31;
+      float mm[6];
+#pragma unroll
+      for (int e = 0; e < 6; ++e) mm[e] = ms[(e * BT + tl) * MS + cl];
+      const float s12 = mm[1] + mm[2], d12 = mm[1] - mm[2], s34 = mm[3] + mm[4], d34 = mm[3] - mm[4];
+      float yv[4];
+      yv[0] = mm[0] + s12 + s34;
+      yv[1] = d12 + 2.f * d34;
+      yv[2] = s12 + 4.f * s34;
+      yv[3] = d12 + 8.f * d34 + mm[5];
+      const float bv = p.bias ? p.bias[cb * BN + pass * 32 + cl] : 0.f;
+#pragma unroll
+      for (int a2 = 0; a2 < 4; ++a2) {
+        float v = yv[a2] + bv + rv[it][a2];
+        if (p.relu) v = fmaxf(v, 0.f);
+        yout[o0[it] + (size_t)a2 * HW * CO] = v;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool winot_supported(const ConvParams& p) {
+  return !p.in_bf16 && !p.out_bf16 && !p.stem && !p.x2 && p.KT == 3 && p.KH == 1 && p.KW == 1 && p.st == 1 &&
+         p.sh == 1 && p.sw == 1 && p.pt == 1 && p.ph == 0 && p.pw == 0 && p.Cin % 8 == 0 && p.Cout % BN == 0 &&
+         p.To == p.Ti && p.Ti % 4 == 0 && p.Ho == p.Hi && p.Wo == p.Wi &&
+         (size_t)p.N * p.Ti * p.Hi * p.Wi * (p.Cin > p.Cout ? p.Cin : p.Cout) < ((size_t)1 << 31);
+}
+
+// U: [Cin/8][6][Cout/64][64][8] transformed weights (winot_transform_weights).
+hipError_t launch_winot(const ConvParams& p, hipStream_t s) {
+  if (!winot_supported(p)) return hipErrorInvalidValue;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)conv_winot, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int n_tiles = p.N * (p.Ti / 4) * p.Hi * p.Wi;
+  const int n_co = p.Cout / BN;
+  const int nb = (n_tiles + BT - 1) / BT;
+  hipLaunchKernelGGL(conv_winot, dim3(nb * n_co), dim3(NTHR), LDS_BYTES, s, p, n_co, n_tiles);
+  return hipGetLastError();
+}
+
+// Host: U[c/8][e][o/64][o%64][c%8] = (G g_{o,c})[e] in double, g = folded 3-tap temporal kernel.
+void winot_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U) {
+  static const double G[6][3] = {{1.0 / 4, 0, 0},
+                                 {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                                 {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                                 {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                                 {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                                 {0, 0, 1}};
+  const int ncb = cout_p / BN;
+  for (size_t i = 0; i < (size_t)6 * cin_p * cout_p; ++i) U[i] = 0.f;
+  for (int o = 0; o < cout; ++o)
+    for (int c = 0; c < cin; ++c) {
+      const double* g = w + ((size_t)o * cin + c) * 3;
+      for (int e = 0; e < 6; ++e) {
+        const double u = G[e][0] * g[0] + G[e][1] * g[1] + G[e][2] * g[2];
+        U[((((size_t)(c / 8) * 6 + e) * ncb + o / BN) * BN + o % BN) * 8 + c % 8] = (float)u;
+      }
+    }
+}
