@@ -27,6 +27,7 @@ METRIC = "32f×112×112 clips/sec at 1/2/4/8 MI355X; Dice Δ vs CPU ref"
 GFLOP_PER_CLIP = 167.59          # algorithmic (comb_1 commuted), SURVEY.md §8(d)
 GFLOP_PER_CLIP_AS_WRITTEN = 218.29
 FP32_PEAK_TFLOPS = 157.3         # MI355X fp32 (vector = MFMA), MI355X_MICROARCH.md
+BF16_PEAK_TFLOPS = 2500.0        # MI355X bf16 MFMA dense
 
 
 def parse():
@@ -101,6 +102,7 @@ def main():
         step()
     torch.cuda.synchronize()
     fwd_events.clear()
+    model.engine.set_kernel_timing(True)  # per-kernel HIP events on the forward's stream
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -111,6 +113,8 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    ktimes = model.engine.kernel_timing()
+    model.engine.set_kernel_timing(False)
     fwd_ms = sum(a.elapsed_time(b) for a, b, _ in fwd_events)
     fwd_clips = sum(n for _, _, n in fwd_events)
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -138,6 +142,7 @@ def main():
         for _ in range(args.warmup):
             step()
         fwd_events.clear()
+        model.engine.set_kernel_timing(True)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -148,6 +153,8 @@ def main():
         if world > 1:
             dist.barrier()
         dt16 = time.perf_counter() - t0
+        k16 = model.engine.kernel_timing()
+        model.engine.set_kernel_timing(False)
         t = torch.tensor([dt16], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -160,6 +167,7 @@ def main():
                 "ms_per_step": round(dt16 / args.steps * 1e3, 3),
                 "forward_ms_per_clip": round(f16_ms / max(f16_clips, 1), 4),
                 "dice_delta_vs_fp32_fused_masks": round(float(max(d16)) if d16 else 0.0, 6),
+                "roofline": kernel_roofline(k16, BF16_PEAK_TFLOPS, "bf16"),
                 "note": "BASELINE config[4]: bf16 activations/weights, fp32 accumulate, fp32 decoder head; "
                         "Dice tolerance 1e-2"}
 
@@ -182,13 +190,13 @@ def main():
                        "videos_per_gpu": args.videos_per_gpu, "frames": args.frames, "fuse": args.fuse,
                        "step": args.step, "clips_per_step": clips_per_step, "batch_size": args.batch_size,
                        "parallelism": f"clip-shard x{world}, all-gather of per-clip logits"},
-            "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
-                         "traffic": (profiled_traffic() or {}).get("bytes_per_forward"),
-                         "traffic_note": "HBM bytes per forward launch sequence (30 clips), rocprofv3 PMC "
-                                         "FETCH_SIZE x2 + WRITE_SIZE from " + str((profiled_traffic() or {}).get("source")),
-                         "kernel": "model forward (clasfv_forward: 41 conv_igemm + decoder launches)",
-                         "gflop_per_clip": GFLOP_PER_CLIP, "forward_ms_per_clip": round(fwd_ms / max(fwd_clips, 1), 4)},
+            "roofline": kernel_roofline(ktimes, FP32_PEAK_TFLOPS, "fp32"),
+            "forward": {"achieved_tflops": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS,
+                        "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "gflop_per_clip": GFLOP_PER_CLIP,
+                        "forward_ms_per_clip": round(fwd_ms / max(fwd_clips, 1), 4),
+                        "note": "whole clasfv_forward (all conv + decoder launches), HIP events around each call"},
+            "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                            "tflops": round(v["gflop"] / max(v["ms"], 1e-9), 2)} for k, v in ktimes.items()},
             "cpu_baseline": cpu,
             "dice_delta_vs_cpu": dice,
             "bf16": bf16,
@@ -199,21 +207,41 @@ def main():
         dist.destroy_process_group()
 
 
-def profiled_traffic():
-    """HBM bytes per forward launch sequence from the committed rocprofv3 PMC summary
-    (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or None."""
+def kernel_roofline(ktimes, peak, dtype):
+    """Roofline object of the dominant kernel (largest summed device time in the timed region):
+    achieved = its algorithmic GFLOP per launch / its mean launch duration (HIP events recorded by
+    the engine on the launch stream), traffic = HBM bytes per launch from the committed rocprofv3
+    PMC summary (profiles/, FETCH_SIZE x2 + WRITE_SIZE) when one exists for this kernel."""
+    if not ktimes:
+        return None
+    name, k = max(ktimes.items(), key=lambda kv: kv[1]["ms"])
+    n = max(k["launches"], 1)
+    tflops = k["gflop"] / max(k["ms"], 1e-9)  # GFLOP/ms = TFLOP/s
+    tr = profiled_traffic(name, dtype)
+    return {"bound": "mfma", "achieved": round(tflops, 3), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(tflops / peak, 4), "traffic": tr and tr["bytes_per_launch"],
+            "kernel": name, "launches": k["launches"], "avg_launch_ms": round(k["ms"] / n, 4),
+            "gflop_per_launch": round(k["gflop"] / n, 3),
+            "traffic_source": tr and tr["source"],
+            "note": "algorithmic GFLOP = direct-convolution MACs x 2 over unpadded channels (Winograd kernels "
+                    "execute fewer MFMA flops than they are credited)"}
+
+
+def profiled_traffic(kernel, dtype):
+    """HBM bytes per launch of `kernel` (averaged over one forward) from the newest committed
+    rocprofv3 PMC summary: 'pmc <kernel> launches=L fetch_mib=F write_mib=W' lines written by
+    tools/prof_summary.py, FETCH already x2-corrected (MI355X_MICROARCH.md HBM section)."""
     import glob
     import re
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_kernel_stats.txt")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_traffic_{dtype}.txt")))
     if not files:
         return None
-    txt = open(files[-1]).read()
-    f = re.search(r"FETCH_SIZE last forward: [\d.]+ MiB raw, x2 corrected = ([\d.]+) MiB", txt)
-    w = re.search(r"WRITE_SIZE last forward: [\d.]+ MiB raw, x1 corrected = ([\d.]+) MiB", txt)
-    if not (f and w):
+    m = re.search(r"^pmc %s launches=(\d+) fetch_mib=([\d.]+) write_mib=([\d.]+)" % re.escape(kernel),
+                  open(files[-1]).read(), re.M)
+    if not m:
         return None
-    return {"bytes_per_forward": int((float(f.group(1)) + float(w.group(1))) * 2**20),
-            "clips_per_forward": 30, "source": os.path.basename(files[-1])}
+    n, f, w = int(m.group(1)), float(m.group(2)), float(m.group(3))
+    return {"bytes_per_launch": int((f + w) * 2**20 / max(n, 1)), "source": os.path.basename(files[-1])}
 
 
 def cpu_baseline(args, S, gpu_model):

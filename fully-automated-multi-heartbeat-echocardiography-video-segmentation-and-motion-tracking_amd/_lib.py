@@ -24,6 +24,9 @@ SIGNATURES = {
     "clasfv_workspace_bytes": (c_int64, [_P]),
     "clasfv_set_compute_dtype": (c_int, [_P, c_int]),
     "clasfv_get_compute_dtype": (c_int, [_P]),
+    "clasfv_set_kernel_timing": (c_int, [_P, c_int]),
+    "clasfv_kernel_timing": (c_int, [_P, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int),
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "clasfv_build_clips": (c_int, [_P, c_int, c_int, c_int, _P, c_int, c_int, _P, _P]),
     "clasfv_pass_labels": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, _P]),
     "clasfv_fuse_votes": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, _P, _P]),

@@ -140,6 +140,16 @@ struct clasfv_engine {
   size_t arena_bytes = 0;
   float* part = nullptr;  // normaliser partials
   float* zero = nullptr;  // 256 zero bytes for padding taps
+  // per-kernel HIP-event timing of clasfv_forward (clasfv_set_kernel_timing)
+  bool ktime = false;
+  std::vector<hipEvent_t> evs;  // event pool; evs[0..nev) recorded since the last read
+  int nev = 0;
+  struct Rec {
+    const char* name;
+    double gflop;
+    int e0, e1;
+  };
+  std::vector<Rec> recs;
 };
 
 namespace {
@@ -269,8 +279,14 @@ struct Shape5 {
   size_t numel() const { return (size_t)n * t * h * w * c; }
 };
 
+// Algorithmic FLOPs of one conv (2 per MAC over the unpadded channels).
+double conv_gflop(const Conv& c, const Shape5& out) {
+  const double m = (double)out.n * out.t * out.h * out.w;
+  return 2.0 * m * c.cout * (double)(c.cin + c.cin2) * c.kt * c.kh * c.kw * 1e-9;
+}
+
 int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
-             hipStream_t s, const void* zero_block, const void* x2 = nullptr) {
+             hipStream_t s, const void* zero_block, const void* x2, const char** kname) {
   out.n = in.n;
   out.t = (in.t + 2 * c.pt - c.kt) / c.st + 1;
   out.h = (in.h + 2 * c.ph - c.kh) / c.sh + 1;
@@ -299,6 +315,7 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
     p.w = c.dwino;
     if (wino_supported(p)) {
       HIP_TRY(launch_wino(p, s));
+      *kname = "conv_wino";
       return CLASFV_OK;
     }
     p.w = c.dw;
@@ -307,6 +324,7 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
     p.w = c.dwinot;
     if (winot_supported(p)) {
       HIP_TRY(launch_winot(p, s));
+      *kname = "conv_winot";
       return CLASFV_OK;
     }
     p.w = c.dw;
@@ -317,6 +335,7 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
     conv_pick_tile(p.M, c.cout_p, force_nt, &mt, &bn);
   }
   HIP_TRY(launch_conv(p, mt, bn, s));
+  *kname = c.stem ? "conv_stem_f32" : "conv_dma";
   return CLASFV_OK;
 }
 
@@ -360,6 +379,17 @@ void make_layout(int N, int T, int H, int W, Layout& L) {
   L.total = o;
 }
 
+// Record one timing event on s (pool grows on demand); returns its index or -1 on failure.
+int tick(clasfv_engine* h, hipStream_t s) {
+  if (h->nev == (int)h->evs.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return -1;
+    h->evs.push_back(e);
+  }
+  if (hipEventRecord(h->evs[h->nev], s) != hipSuccess) return -1;
+  return h->nev++;
+}
+
 float tap_scale(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
 
 }  // namespace
@@ -399,6 +429,7 @@ int clasfv_destroy(clasfv_t h) {
   (void)hipFree(h->arena);
   (void)hipFree(h->part);
   (void)hipFree(h->zero);
+  for (auto e : h->evs) (void)hipEventDestroy(e);
   delete h;
   return CLASFV_OK;
 }
@@ -572,13 +603,28 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
     h->arena_bytes = L.total;
   }
   auto buf = [&](int b) { return reinterpret_cast<void*>(h->arena + L.off[b]); };
+  int last_ev = h->ktime ? tick(h, s) : -1;
+  auto timed = [&](const char* name, double gflop) {
+    if (last_ev < 0) return;
+    const int e = tick(h, s);
+    if (e >= 0) h->recs.push_back({name, gflop, last_ev, e});
+    last_ev = e;
+  };
+  auto run = [&](const Conv& c, const void* xin, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
+                 const void* x2 = nullptr) {
+    const char* kname = "";
+    int rc_ = run_conv(c, xin, in, y, out, res, relu, s, h->zero, x2, &kname);
+    if (!rc_) timed(kname, conv_gflop(c, out));
+    return rc_;
+  };
 
   HIP_TRY(launch_pack_input(x, reinterpret_cast<float*>(buf(XIN)), N, T, H * W, s));
+  timed("pack_input_kernel", 0.0);
   Shape5 sx{N, T, H, W, 4}, s0, sx0;
   int rc;
   size_t ci = 0;
-  if ((rc = run_conv(h->convs[ci++], buf(XIN), sx, buf(S0), s0, nullptr, true, s, h->zero))) return rc;
-  if ((rc = run_conv(h->convs[ci++], buf(S0), s0, buf(X0), sx0, nullptr, true, s, h->zero))) return rc;
+  if ((rc = run(h->convs[ci++], buf(XIN), sx, buf(S0), s0, nullptr, true))) return rc;
+  if ((rc = run(h->convs[ci++], buf(S0), s0, buf(X0), sx0, nullptr, true))) return rc;
   const int outs[4][2] = {{L1A, L1}, {L2A, L2}, {L3A, L3}, {L4A, L4}};
   void* cur = buf(X0);
   Shape5 cs = sx0, taps_shape[5];
@@ -593,16 +639,16 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
       const Conv& tp2 = h->convs[ci++];
       const Conv* ds = (ci < h->convs.size() && h->convs[ci].role == DS) ? &h->convs[ci++] : nullptr;
       Shape5 sm, sa, sm2, so, sd;
-      if ((rc = run_conv(sp1, cur, cs, buf(MID), sm, nullptr, true, s, h->zero))) return rc;
-      if ((rc = run_conv(tp1, buf(MID), sm, buf(TA), sa, nullptr, true, s, h->zero))) return rc;
-      if ((rc = run_conv(sp2, buf(TA), sa, buf(MID), sm2, nullptr, true, s, h->zero))) return rc;
+      if ((rc = run(sp1, cur, cs, buf(MID), sm, nullptr, true))) return rc;
+      if ((rc = run(tp1, buf(MID), sm, buf(TA), sa, nullptr, true))) return rc;
+      if ((rc = run(sp2, buf(TA), sa, buf(MID), sm2, nullptr, true))) return rc;
       const void* res = cur;
       if (ds) {
-        if ((rc = run_conv(*ds, cur, cs, buf(DSB), sd, nullptr, false, s, h->zero))) return rc;
+        if ((rc = run(*ds, cur, cs, buf(DSB), sd, nullptr, false))) return rc;
         res = buf(DSB);
       }
       void* out = buf(outs[li][b]);
-      if ((rc = run_conv(tp2, buf(MID), sm2, out, so, res, true, s, h->zero))) return rc;
+      if ((rc = run(tp2, buf(MID), sm2, out, so, res, true))) return rc;
       cur = out;
       cs = so;
     }
@@ -611,11 +657,11 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   }
   // decoder projections at tap resolution: P01 = W0 f0 + W1 f1, P2..P4
   Shape5 sp;
-  if ((rc = run_conv(h->proj[0], taps[0], taps_shape[0], buf(P01), sp, nullptr, false, s, h->zero, taps[1]))) return rc;
+  if ((rc = run(h->proj[0], taps[0], taps_shape[0], buf(P01), sp, nullptr, false, taps[1]))) return rc;
   Shape5 sp2, sp3, sp4;
-  if ((rc = run_conv(h->proj[2], taps[2], taps_shape[2], buf(PP2), sp2, nullptr, false, s, h->zero))) return rc;
-  if ((rc = run_conv(h->proj[3], taps[3], taps_shape[3], buf(PP3), sp3, nullptr, false, s, h->zero))) return rc;
-  if ((rc = run_conv(h->proj[4], taps[4], taps_shape[4], buf(PP4), sp4, nullptr, false, s, h->zero))) return rc;
+  if ((rc = run(h->proj[2], taps[2], taps_shape[2], buf(PP2), sp2, nullptr, false))) return rc;
+  if ((rc = run(h->proj[3], taps[3], taps_shape[3], buf(PP3), sp3, nullptr, false))) return rc;
+  if ((rc = run(h->proj[4], taps[4], taps_shape[4], buf(PP4), sp4, nullptr, false))) return rc;
 
   DecParams d;
   const Shape5 tsh[4] = {sp, sp2, sp3, sp4};
@@ -638,7 +684,41 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   d.mot = mot;
   d.N = N, d.T = T, d.H = H, d.W = W;
   HIP_TRY(launch_decoder(d, s));
+  timed("decoder_kernel", 2.0 * N * (double)T * H * W * (64 * 64 + 64 * 6) * 1e-9);
   return CLASFV_OK;
+}
+
+int clasfv_set_kernel_timing(clasfv_t h, int enable) {
+  if (!h) return fail(CLASFV_EINVAL, "null handle");
+  h->ktime = enable != 0;
+  h->recs.clear();
+  h->nev = 0;
+  return CLASFV_OK;
+}
+
+int clasfv_kernel_timing(clasfv_t h, int cap, const char** names, int* launches, double* ms, double* gflop) {
+  if (!h || cap < 0 || (cap > 0 && (!names || !launches || !ms || !gflop))) return fail(CLASFV_EINVAL, "bad argument");
+  if (h->nev > 0) HIP_TRY(hipEventSynchronize(h->evs[h->nev - 1]));
+  int n = 0;
+  for (const auto& r : h->recs) {
+    float t = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t, h->evs[r.e0], h->evs[r.e1]));
+    int i = 0;
+    while (i < n && strcmp(names[i], r.name) != 0) ++i;
+    if (i == n) {
+      if (n == cap) return fail(CLASFV_EINVAL, "kernel timing: cap too small");
+      names[n] = r.name;
+      launches[n] = 0;
+      ms[n] = gflop[n] = 0.0;
+      ++n;
+    }
+    launches[i] += 1;
+    ms[i] += t;
+    gflop[i] += r.gflop;
+  }
+  h->recs.clear();
+  h->nev = 0;
+  return n;
 }
 
 int clasfv_build_clips(const float* video, int T, int H, int W, const int32_t* table, int n, int interp, float* clips,

@@ -76,6 +76,22 @@ class Engine:
         _lib.check(self.lib.clasfv_forward(self.h, _lib.ptr(x), n, t, hh, ww, _lib.ptr(seg), _lib.ptr(mot),
                                            _lib.stream_ptr(stream)), "clasfv_forward")
 
+    def set_kernel_timing(self, enable=True):
+        """Per-kernel HIP-event timing of every later forward (see clasfv_kernel_timing)."""
+        _lib.check(self.lib.clasfv_set_kernel_timing(self.h, 1 if enable else 0), "clasfv_set_kernel_timing")
+
+    def kernel_timing(self, cap=16):
+        """{kernel: {"launches", "ms", "gflop"}} over the forwards since the last call (then cleared)."""
+        names = (ctypes.c_char_p * cap)()
+        launches = (ctypes.c_int * cap)()
+        ms = (ctypes.c_double * cap)()
+        gf = (ctypes.c_double * cap)()
+        n = self.lib.clasfv_kernel_timing(self.h, cap, names, launches, ms, gf)
+        if n < 0:
+            _lib.check(n, "clasfv_kernel_timing")
+        return {names[i].decode(): {"launches": int(launches[i]), "ms": float(ms[i]), "gflop": float(gf[i])}
+                for i in range(n)}
+
     def workspace_bytes(self):
         return int(self.lib.clasfv_workspace_bytes(self.h))
 

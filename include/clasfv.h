@@ -72,6 +72,18 @@ int64_t clasfv_workspace_bytes(clasfv_t h);
 int clasfv_set_compute_dtype(clasfv_t h, int dtype);
 int clasfv_get_compute_dtype(clasfv_t h);
 
+/* ---- instrumentation (bench.py's live roofline; not on the reference's interface) ------------ */
+/* enable != 0: every later clasfv_forward records one HIP event on its stream before its first
+ * launch and one after each launch, so each kernel's device time is the gap between two events.
+ * Enabling or disabling drops what was recorded. */
+int clasfv_set_kernel_timing(clasfv_t h, int enable);
+/* Waits for the recorded events, aggregates the launches recorded since the last call per kernel
+ * and clears them. Entry i: names[i] (static string, e.g. "conv_wino"), launches[i], ms[i] (summed
+ * device time), gflop[i] (summed algorithmic GFLOP, 2 per MAC over unpadded channels). Returns
+ * the number of entries (<= cap) or a negative error code. */
+int clasfv_kernel_timing(clasfv_t h, int cap, const char** names, int* launches, double* ms,
+                         double* gflop);
+
 /* ---- clip plumbing: replaces src/fuse_utils.py:16-100 ----------------------------------------- */
 /* Build n clips (n,3,32,H,W) from the normalised video (3,T,H,W). Clip i is frames
  * [table[2i+1], table[2i+1]+32) of the temporally shifted video video[:, table[2i]:], resampled

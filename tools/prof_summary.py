@@ -12,15 +12,29 @@ import sys
 from collections import defaultdict
 
 
+KNOWN = ("conv_winot", "conv_wino", "conv_dma", "conv_stem_f32", "pack_input_kernel", "decoder_kernel",
+         "preprocess_video_kernel")
+
+
+def short(name):
+    """Kernel name without template arguments (rocprofv3 -T leaves some templates mangled)."""
+    for k in KNOWN:
+        if k in name:
+            return k
+    return name
+
+
 def kernels(db):
     c = sqlite3.connect(db)
-    return list(c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x from kernels order by start"))
+    return [(short(r[0]),) + tuple(r[1:]) for r in
+            c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x from kernels order by start")]
 
 
 def pmc(db, counter):
     c = sqlite3.connect(db)
-    return list(c.execute("select kernel_name, value from counters_collection where counter_name=? order by dispatch_id",
-                          (counter,)))
+    return [(short(n), v) for n, v in
+            c.execute("select kernel_name, value from counters_collection where counter_name=? order by dispatch_id",
+                      (counter,))]
 
 
 def forwards(seq, name_of=lambda r: r[0]):
@@ -66,7 +80,20 @@ def main():
                 print(f"\n{cn} last forward: {kb / 1024:.1f} MiB raw, x{corr:g} corrected = {kb * corr / 1024:.1f} MiB")
                 conv_kb = sum(v for n, v in fws[-1] if "conv_" in n)
                 dec_kb = sum(v for n, v in fws[-1] if n.startswith("decoder"))
-                print(f"  conv_igemm {conv_kb * corr / 1024:.1f} MiB, decoder {dec_kb * corr / 1024:.1f} MiB")
+                print(f"  conv kernels {conv_kb * corr / 1024:.1f} MiB, decoder {dec_kb * corr / 1024:.1f} MiB")
+        # per-kernel lines for bench.py (profiled_traffic): bytes of the last forward's launches
+        per = defaultdict(lambda: [0, 0.0, 0.0])
+        for col, db, corr in ((1, sys.argv[2], 2.0), (2, sys.argv[3], 1.0)):
+            fws = forwards(pmc(db, "FETCH_SIZE" if col == 1 else "WRITE_SIZE"))
+            if not fws:
+                continue
+            for n, v in fws[-1]:
+                per[n][col] += v * corr / 1024
+                if col == 1:
+                    per[n][0] += 1
+        print()
+        for n, (cnt, f, w) in sorted(per.items(), key=lambda kv: -(kv[1][1] + kv[1][2])):
+            print(f"pmc {n} launches={cnt} fetch_mib={f:.1f} write_mib={w:.1f}")
 
 
 if __name__ == "__main__":
