@@ -753,6 +753,13 @@ int clasfv_warp(const float* img, int N, int C, int H, int W, const float* motio
   return CLASFV_OK;
 }
 
+int clasfv_preprocess_video(const uint8_t* frames, int T, int Hs, int Ws, int H, int W, float* out, void* stream) {
+  if (!frames || !out || T < 1 || Hs < 1 || Ws < 1 || H < 1 || W < 1 || H > 65535 || T > 65535)
+    return fail(CLASFV_EINVAL, "bad argument");
+  HIP_TRY(launch_preprocess_video(frames, T, Hs, Ws, H, W, out, (hipStream_t)stream));
+  return CLASFV_OK;
+}
+
 int clasfv_zeroone_normalize(float* video, int64_t n, void* stream) {
   if (!video || n < 1) return fail(CLASFV_EINVAL, "bad argument");
   static thread_local float* part = nullptr;  // per-thread partials buffer (3 x 512 x 2 floats)

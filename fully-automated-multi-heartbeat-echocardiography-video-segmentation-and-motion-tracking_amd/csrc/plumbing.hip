@@ -5,6 +5,7 @@
 //   fuse_votes         per-frame label fusion            src/fuse_utils.py:82-100
 //   warp               generate_2dmotion_field + grid_sample   src/transform_utils.py:14-34
 //   zeroone_normalize  zeroone_normalizer                src/echonet_dataset.py:38-50
+//   preprocess_video   frames -> (3,T,H,W) + trilinear resize   motion_segment.py:96-106
 //
 // Interpolation arithmetic follows PyTorch's CPU upsample kernel bit for bit (checked against
 // F.interpolate in tests): scale = (float)in/out, src = fma(scale, dst + 0.5, -0.5) clamped at 0,
@@ -13,6 +14,11 @@
 
 #include "common.h"
 #include "plumbing.h"
+
+// Every fused multiply-add below is written out (fmaf) where PyTorch's CPU kernels contract one;
+// nothing else may be contracted (HIP's __fmul_rn etc. are plain operators defined in a header this pragma does not reach, so
+// the operators are written out here).
+#pragma clang fp contract(off)
 
 namespace {
 
@@ -41,7 +47,7 @@ __device__ inline Lin lin_ac_false(int t_in, int t_out, int dst) {
   return r;
 }
 
-__device__ inline float lerp_t(float a, float b, float l0, float l1) { return fmaf(a, l0, __fmul_rn(b, l1)); }
+__device__ inline float lerp_t(float a, float b, float l0, float l1) { return fmaf(a, l0, (b * l1)); }
 
 // ---- build_clips ------------------------------------------------------------------------------
 __global__ void build_clips_kernel(const float* __restrict__ video, int T, int HW, const int32_t* __restrict__ table,
@@ -230,18 +236,24 @@ __global__ __launch_bounds__(SIMPLE_THREADS) void fuse_simple_kernel(const uint8
 }
 
 // ---- warp ------------------------------------------------------------------------------------
-// torch.linspace(-1, 1, n) on the CPU: step = 2/(n-1); first half start + step*i, second half
-// end - step*(n-1-i).
+// torch.linspace(-1, 1, n) on the CPU: step = 2/(n-1); first half fma(step, i, -1), second half
+// fma(-step, n-1-i, 1) (the kernel is built with FMA contraction).
 __device__ inline float linspace_pm1(int i, int n) {
   if (n == 1) return -1.f;
   const float step = 2.0f / (float)(n - 1);
-  return (i < n / 2) ? (-1.f + step * (float)i) : (1.f - step * (float)(n - 1 - i));
+  return (i < n / 2) ? fmaf(step, (float)i, -1.f) : fmaf(-step, (float)(n - 1 - i), 1.f);
 }
 
+// F.grid_sample(bilinear, border, align_corners=False) as PyTorch's vectorised CPU kernel computes it
+// (GridSamplerKernel.cpp, built with FMA contraction; bit-exact vs the reference golden):
+// ix = fma(gx + 1, W/2, -0.5) clipped to [0, W-1]; corner weights nw = s*e, ne = s*w, sw = n*e, se = n*w
+// with w = ix - floor(ix), e = floor(ix) + 1 - ix (same in y); value = fma(se_v, se, fma(sw_v, sw,
+// fma(ne_v, ne, nw_v * nw))), out-of-range corners read as 0.
 __global__ void warp_kernel(const float* __restrict__ img, int N, int C, int H, int W, const float* __restrict__ motion,
                             int64_t m_sn, int64_t m_sc, float* __restrict__ out) {
   const size_t HW = (size_t)H * W;
   const size_t total = (size_t)N * HW;
+  const float sx = (float)W * 0.5f, sy = (float)H * 0.5f;
   for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < total; g += (size_t)gridDim.x * blockDim.x) {
     const int n = (int)(g / HW);
     const int pix = (int)(g - (size_t)n * HW);
@@ -249,26 +261,59 @@ __global__ void warp_kernel(const float* __restrict__ img, int N, int C, int H, 
     const float* mp = motion + n * m_sn + pix;
     const float gx = linspace_pm1(j, W) + mp[0];
     const float gy = linspace_pm1(i, H) + mp[m_sc];
-    // grid_sampler_compute_source_index: unnormalise (align_corners=False), border clip
-    float ix = __fdiv_rn(__fsub_rn(__fmul_rn(__fadd_rn(gx, 1.f), (float)W), 1.f), 2.f);
-    float iy = __fdiv_rn(__fsub_rn(__fmul_rn(__fadd_rn(gy, 1.f), (float)H), 1.f), 2.f);
-    ix = fminf((float)(W - 1), fmaxf(ix, 0.f));
-    iy = fminf((float)(H - 1), fmaxf(iy, 0.f));
+    const float ix = fminf((float)(W - 1), fmaxf(fmaf(gx + 1.f, sx, -0.5f), 0.f));
+    const float iy = fminf((float)(H - 1), fmaxf(fmaf(gy + 1.f, sy, -0.5f), 0.f));
     const float fx0 = floorf(ix), fy0 = floorf(iy);
     const int x0 = (int)fx0, y0 = (int)fy0, x1 = x0 + 1, y1 = y0 + 1;
-    const float wnw = __fmul_rn(fx0 + 1.f - ix, fy0 + 1.f - iy);
-    const float wne = __fmul_rn(ix - fx0, fy0 + 1.f - iy);
-    const float wsw = __fmul_rn(fx0 + 1.f - ix, iy - fy0);
-    const float wse = __fmul_rn(ix - fx0, iy - fy0);
+    const float we = ix - fx0, ee = (fx0 + 1.f) - ix, wn = iy - fy0, ws = (fy0 + 1.f) - iy;
+    const float wnw = ws * ee, wne = ws * we, wsw = wn * ee, wse = wn * we;
     const bool in_x1 = x1 < W, in_y1 = y1 < H;
     for (int c = 0; c < C; ++c) {
       const float* src = img + ((size_t)n * C + c) * HW;
-      float v = __fmul_rn(src[y0 * W + x0], wnw);
-      if (in_x1) v = __fadd_rn(v, __fmul_rn(src[y0 * W + x1], wne));
-      if (in_y1) v = __fadd_rn(v, __fmul_rn(src[y1 * W + x0], wsw));
-      if (in_x1 && in_y1) v = __fadd_rn(v, __fmul_rn(src[y1 * W + x1], wse));
-      out[((size_t)n * C + c) * HW + pix] = v;
+      const float vnw = src[y0 * W + x0];
+      const float vne = in_x1 ? src[y0 * W + x1] : 0.f;
+      const float vsw = in_y1 ? src[y1 * W + x0] : 0.f;
+      const float vse = (in_x1 && in_y1) ? src[y1 * W + x1] : 0.f;
+      out[((size_t)n * C + c) * HW + pix] = fmaf(vse, wse, fmaf(vsw, wsw, fmaf(vne, wne, vnw * wnw)));
     }
+  }
+}
+
+// ---- preprocess_video ---------------------------------------------------------------------------
+// motion_segment.py:96-106: (T,Hs,Ws,3) uint8 RGB frames -> (3,T,Hs,Ws) float32 -> F.interpolate(
+// size=(T,H,W), mode="trilinear", align_corners=True). T is unchanged, so the temporal weights are
+// (1, 0) and that level is the identity; per spatial axis PyTorch's CPU kernel computes
+// src = scale * dst with scale = (float)(in-1)/(out-1), i0 = min((int)src, in-1), l1 = clamp(src - i0),
+// l0 = 1 - l1, and combines W first, then H, as fma(x0, l0, x1 * l1) at each level (bit-exact vs
+// F.interpolate on the CPU; tests/test_oracle.py, tests/test_gpu.py).
+__device__ inline Lin lin_ac_true(int n_in, float scale, int dst) {
+  Lin r;
+  const float src = (scale * (float)dst);
+  r.i0 = min((int)src, n_in - 1);
+  r.l1 = fminf(fmaxf((src - (float)r.i0), 0.f), 1.f);
+  r.i1 = r.i0 + (r.i0 < n_in - 1 ? 1 : 0);
+  r.l0 = (1.f - r.l1);
+  return r;
+}
+
+__global__ void preprocess_video_kernel(const uint8_t* __restrict__ frames, int T, int Hs, int Ws, int H, int W,
+                                        float sh, float sw, float* __restrict__ out) {
+  const int t = blockIdx.z, y = blockIdx.y;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= W) return;
+  const Lin ly = lin_ac_true(Hs, sh, y), lx = lin_ac_true(Ws, sw, x);
+  const uint8_t* f = frames + (size_t)t * Hs * Ws * 3;
+  const uint8_t* r0 = f + (size_t)ly.i0 * Ws * 3;
+  const uint8_t* r1 = f + (size_t)ly.i1 * Ws * 3;
+  const size_t plane = (size_t)T * H * W;
+  float* o = out + ((size_t)t * H + y) * W + x;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float a = r0[lx.i0 * 3 + c], b = r0[lx.i1 * 3 + c];
+    const float cc = r1[lx.i0 * 3 + c], d = r1[lx.i1 * 3 + c];
+    const float top = lerp_t(a, b, lx.l0, lx.l1);
+    const float bot = lerp_t(cc, d, lx.l0, lx.l1);
+    o[c * plane] = lerp_t(top, bot, ly.l0, ly.l1);
   }
 }
 
@@ -314,13 +359,13 @@ __global__ void normalize_kernel(float* __restrict__ v, int64_t n, const float* 
       hi = fmaxf(hi, part[(c * nparts + b) * 2 + 1]);
     }
     s_lo = lo;
-    s_den = __fsub_rn(hi, lo);  // == max over the channel of (x - min): subtraction is monotone
+    s_den = (hi - lo);  // == max over the channel of (x - min): subtraction is monotone
   }
   __syncthreads();
   const float lo = s_lo, den = s_den;
   float* x = v + (size_t)c * n;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    x[i] = __fdiv_rn(__fsub_rn(x[i], lo), den);
+    x[i] = ((x[i] - lo) / den);
 }
 
 inline int blocks_for(size_t n, int per_block, int cap) {
@@ -377,3 +422,13 @@ hipError_t launch_zeroone_normalize(float* v, int64_t n, float* part, hipStream_
 }
 
 int zeroone_partials_floats() { return 3 * RED_BLOCKS * 2; }
+
+hipError_t launch_preprocess_video(const uint8_t* frames, int T, int Hs, int Ws, int H, int W, float* out,
+                                   hipStream_t s) {
+  // align_corners=True scales in host float arithmetic, as at::native::area_pixel_compute_scale
+  const float sh = H > 1 ? (float)(Hs - 1) / (float)(H - 1) : 0.f;
+  const float sw = W > 1 ? (float)(Ws - 1) / (float)(W - 1) : 0.f;
+  dim3 grid((W + 127) / 128, H, T);
+  hipLaunchKernelGGL(preprocess_video_kernel, grid, dim3(128), 0, s, frames, T, Hs, Ws, H, W, sh, sw, out);
+  return hipGetLastError();
+}

@@ -110,7 +110,12 @@ int clasfv_fuse_votes(const uint8_t* labels_dev, int K, int T, int step, int H, 
 int clasfv_warp(const float* img_dev, int N, int C, int H, int W, const float* motion_dev, int64_t m_sn,
                 int64_t m_sc, float* out_dev, void* stream);
 
-/* ---- preprocessing (src/echonet_dataset.py:38-50) ------------------------------------------------ */
+/* ---- preprocessing (motion_segment.py:96-106, src/echonet_dataset.py:38-50) --------------------- */
+/* frames_dev (T,Hs,Ws,3) uint8 RGB -> out_dev (3,T,H,W) float32, resized as
+ * F.interpolate(size=(T,H,W), mode="trilinear", align_corners=True) on the (1,3,T,Hs,Ws) float
+ * video (bit-exact vs PyTorch's CPU kernel). Not normalised: follow with clasfv_zeroone_normalize. */
+int clasfv_preprocess_video(const uint8_t* frames_dev, int T, int Hs, int Ws, int H, int W, float* out_dev,
+                            void* stream);
 /* In place: per channel c of video (3, n_per_channel) subtract the channel min, divide by the max. */
 int clasfv_zeroone_normalize(float* video_dev, int64_t n_per_channel, void* stream);
 

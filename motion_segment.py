@@ -16,7 +16,6 @@ import sys
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -78,7 +77,7 @@ def main(argv=None):
     from clasfv_amd.echo import compute_ef_using_putative_clips
     from clasfv_amd.fuse_utils import segment_a_video_with_fusion
     from clasfv_amd.model import R2plus1D_18_MotionNet
-    from clasfv_amd.preprocess import zeroone_normalize_
+    from clasfv_amd.preprocess import preprocess_video
     from clasfv_amd.weights import DEFAULT_SEED, load_checkpoint
 
     seed = args.synthetic_weights if args.synthetic_weights is not None else DEFAULT_SEED
@@ -89,12 +88,8 @@ def main(argv=None):
         print(f"R2+1D MotionNet has {sum(p.numel() for p in model.parameters() if p.requires_grad)} parameters.")
     model.eval()
 
-    video = read_video(args.path)
-    video = torch.from_numpy(video.transpose((3, 0, 1, 2)).astype(np.float32)).to(dev)
-    if video.shape[2:] != (args.height, args.width):  # motion_segment.py:100-104
-        video = F.interpolate(video[None], size=(video.shape[1], args.height, args.width), mode="trilinear",
-                              align_corners=True)[0]
-    video = zeroone_normalize_(video.contiguous())
+    # motion_segment.py:96-106 on the device: uint8 frames -> resize -> zero-one normalisation
+    video = preprocess_video(read_video(args.path), args.height, args.width, device=dev)
 
     segmentations = segment_a_video_with_fusion(video, model=model, interpolate_last=True, step=args.step,
                                                 num_clips=args.fuse, fuse_method=args.fuse_method, class_list=[0, 1],

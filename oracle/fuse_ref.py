@@ -52,6 +52,30 @@ def temporal_resample(x, t_out, axis=1):
     return _fma(a, l0, (b * l1).astype(np.float32))
 
 
+def _ac_true_index(n_in, n_out):
+    """align_corners=True linear weights: scale = (float)(in-1)/(out-1), src = scale*dst (float32)."""
+    scale = np.float32(np.float32(n_in - 1) / np.float32(n_out - 1)) if n_out > 1 else np.float32(0)
+    src = (scale * np.arange(n_out).astype(np.float32)).astype(np.float32)
+    i0 = np.minimum(src.astype(np.int64), n_in - 1)
+    l1 = np.clip(src - i0.astype(np.float32), np.float32(0), np.float32(1)).astype(np.float32)
+    return i0, i0 + (i0 < n_in - 1), (np.float32(1) - l1).astype(np.float32), l1
+
+
+def preprocess_frames(frames, height=112, width=112):
+    """motion_segment.py:96-104: (T,Hs,Ws,3) uint8 -> (3,T,Hs,Ws) float32 -> F.interpolate(size=(T,
+    height, width), mode="trilinear", align_corners=True). The temporal level is the identity (T kept);
+    W then H are combined as fma(x0, l0, x1*l1) (PyTorch's CPU Interpolate<>::eval, bit-exact).
+    Not normalised (zeroone_normalizer follows in the reference)."""
+    x = np.asarray(frames).transpose(3, 0, 1, 2).astype(np.float32)
+    h0, h1, lh0, lh1 = _ac_true_index(x.shape[2], height)
+    w0, w1, lw0, lw1 = _ac_true_index(x.shape[3], width)
+    rows0, rows1 = x[:, :, h0], x[:, :, h1]
+    lw0, lw1 = lw0[None, None, None, :], lw1[None, None, None, :]
+    top = _fma(rows0[..., w0], lw0, (rows0[..., w1] * lw1).astype(np.float32))
+    bot = _fma(rows1[..., w0], lw0, (rows1[..., w1] * lw1).astype(np.float32))
+    return _fma(top, lh0[None, None, :, None], (bot * lh1[None, None, :, None]).astype(np.float32))
+
+
 def _fma(x, y, z):
     """float32 fused multiply-add emulated in float64 (exact product, one final rounding)."""
     return (np.asarray(x, np.float64) * np.asarray(y, np.float64) + np.asarray(z, np.float64)).astype(np.float32)

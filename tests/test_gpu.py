@@ -176,15 +176,40 @@ def test_normalizer_bitexact_vs_reference_golden():
     np.testing.assert_allclose(out.astype(np.float64).sum((1, 2, 3)), g["out_sum"], rtol=1e-12)
 
 
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_preprocess_video_bitexact_vs_reference_golden(case):
+    """clasfv_preprocess_video + normaliser == the reference CLI's resize + zeroone_normalizer."""
+    import clasfv_amd.synthetic as S
+    from clasfv_amd.preprocess import preprocess_video
+    g = golden("preprocess.npz")
+    T, Hs, Ws, seed = (int(v) for v in g[f"case{case}"])
+    frames = S.echo_video_uint8(T, Hs, Ws, seed=seed)
+    r = preprocess_video(frames, normalize=False).cpu().numpy()
+    np.testing.assert_array_equal(r[:, ::2, ::3, ::5], g[f"resized{case}_sample"])
+    np.testing.assert_array_equal(r, fuse_ref.preprocess_frames(frames))
+    n = preprocess_video(torch.from_numpy(frames).cuda()).cpu().numpy()
+    np.testing.assert_array_equal(n[:, ::2, ::3, ::5], g[f"norm{case}_sample"])
+    np.testing.assert_allclose(n.astype(np.float64).sum((1, 2, 3)), g[f"norm{case}_sum"], rtol=1e-12)
+
+
+@pytest.mark.parametrize("shape", [(4, 600, 800, 112, 112), (3, 50, 60, 64, 96), (2, 1, 7, 5, 9), (200, 112, 112, 112, 112)])
+def test_preprocess_video_bitexact_vs_oracle(shape):
+    from clasfv_amd.preprocess import preprocess_video
+    T, Hs, Ws, H, W = shape
+    v = np.random.default_rng(sum(shape)).integers(0, 256, (T, Hs, Ws, 3), dtype=np.uint8)
+    out = preprocess_video(v, H, W, normalize=False).cpu().numpy()
+    np.testing.assert_array_equal(out, fuse_ref.preprocess_frames(v, H, W))
+
+
 def test_warp_vs_reference_golden():
     from clasfv_amd.warp import warp
     g = golden("warp.npz")
     for name in ("zero", "plus5px", "minus5px_y", "random", "large"):
         img = g["img_r"] if name in ("random", "large") else g["img"]
         out = warp(torch.from_numpy(img).cuda(), torch.from_numpy(g["flow_" + name]).cuda()).cpu().numpy()
-        np.testing.assert_allclose(out, g["out_" + name], atol=2e-5, err_msg=name)
+        np.testing.assert_array_equal(out, g["out_" + name], err_msg=name)  # bit-exact
     box = warp(torch.from_numpy(g["box"]).cuda(), torch.zeros(1, 2, 112, 112).cuda()).cpu().numpy()
-    np.testing.assert_allclose(box, g["box_zero"], atol=2e-5)
+    np.testing.assert_array_equal(box, g["box_zero"])
 
 
 def test_warp_strided_motion_slice_vs_oracle():
@@ -194,7 +219,7 @@ def test_warp_strided_motion_slice_vs_oracle():
     motion = torch.from_numpy(np.tanh(rng.normal(0, 0.2, (2, 4, 5, 40, 56))).astype(np.float32))
     out = warp(img.cuda(), motion.cuda()[:, 2:, 3]).cpu()
     ref = warp_ref.warp(img, motion[:, 2:, 3])
-    np.testing.assert_allclose(out.numpy(), ref.numpy(), atol=2e-5)
+    np.testing.assert_array_equal(out.numpy(), ref.numpy())
 
 
 def test_cli_end_to_end(tmp_path):

@@ -141,3 +141,27 @@ def test_chunked_oracle_equals_as_written(synthetic_sd):
     s2, m2 = r2plus1d_ref.forward_chunked(synthetic_sd, x, frames_per_chunk=3)
     np.testing.assert_allclose(s2.numpy(), s1.numpy(), atol=2e-5)
     np.testing.assert_allclose(m2.numpy(), m1.numpy(), atol=1e-6)
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_preprocess_oracle_matches_reference(case):
+    """motion_segment.py:96-106 replayed on the reference (tests/golden/make_golden_preprocess.py):
+    the numpy restatement of the trilinear resize is bit-exact, and with the normaliser too."""
+    import clasfv_amd.synthetic as S
+    g = golden("preprocess.npz")
+    T, Hs, Ws, seed = (int(v) for v in g[f"case{case}"])
+    r = fuse_ref.preprocess_frames(S.echo_video_uint8(T, Hs, Ws, seed=seed))
+    np.testing.assert_array_equal(r[:, ::2, ::3, ::5], g[f"resized{case}_sample"])
+    np.testing.assert_allclose(r.astype(np.float64).sum((1, 2, 3)), g[f"resized{case}_sum"], rtol=1e-12)
+    n = fuse_ref.zeroone_normalizer(r)
+    np.testing.assert_array_equal(n[:, ::2, ::3, ::5], g[f"norm{case}_sample"])
+    np.testing.assert_allclose(n.astype(np.float64).sum((1, 2, 3)), g[f"norm{case}_sum"], rtol=1e-12)
+
+
+@pytest.mark.parametrize("shape", [(3, 37, 53, 112, 112), (2, 600, 800, 112, 112), (2, 50, 60, 64, 96), (2, 1, 7, 5, 9)])
+def test_preprocess_oracle_bitexact_vs_torch(shape):
+    T, Hs, Ws, H, W = shape
+    v = np.random.default_rng(sum(shape)).integers(0, 256, (T, Hs, Ws, 3), dtype=np.uint8)
+    ref = F.interpolate(torch.from_numpy(v.transpose(3, 0, 1, 2).astype(np.float32))[None], size=(T, H, W),
+                        mode="trilinear", align_corners=True)[0].numpy()
+    np.testing.assert_array_equal(fuse_ref.preprocess_frames(v, H, W), ref)

@@ -8,9 +8,10 @@ groups=(
  "TCC_HIT_sum TCC_MISS_sum"
  "TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum"
  "TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum"
+ "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE"
 )
 i=0
 for g in "${groups[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $g -T -d $out/g$i -o p -- python3 bench.py --steps 1 --warmup 1 --cpu-baseline 0 --dtype $dt --extra-bf16 0 > $out/g$i.log 2>&1 || { echo "group $i failed"; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $g -T -d $out/g$i -o p -- python3 bench.py --steps 1 --warmup 1 --cpu-baseline 0 --dtype $dt --extra-bf16 0 --fuse 1 > $out/g$i.log 2>&1 || { echo "group $i failed"; exit 1; }
 done
