@@ -32,6 +32,7 @@ SIGNATURES = {
     "clasfv_fuse_votes": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, _P, _P]),
     "clasfv_warp": (c_int, [_P, c_int, c_int, c_int, c_int, _P, c_int64, c_int64, _P, _P]),
     "clasfv_zeroone_normalize": (c_int, [_P, c_int64, _P]),
+    "clasfv_warp_backward": (c_int, [_P, _P, c_int, c_int, c_int, c_int, _P, c_int64, c_int64, _P, _P, _P]),
     "clasfv_preprocess_video": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, _P, _P]),
 }
 

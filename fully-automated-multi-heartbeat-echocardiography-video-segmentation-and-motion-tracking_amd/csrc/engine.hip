@@ -753,6 +753,15 @@ int clasfv_warp(const float* img, int N, int C, int H, int W, const float* motio
   return CLASFV_OK;
 }
 
+int clasfv_warp_backward(const float* grad_out, const float* img, int N, int C, int H, int W, const float* motion,
+                         int64_t m_sn, int64_t m_sc, float* grad_img, float* grad_motion, void* stream) {
+  if (!grad_out || !img || !motion || (!grad_img && !grad_motion) || N < 1 || C < 1 || H < 1 || W < 1)
+    return fail(CLASFV_EINVAL, "bad argument");
+  HIP_TRY(launch_warp_backward(grad_out, img, N, C, H, W, motion, m_sn, m_sc, grad_img, grad_motion,
+                               (hipStream_t)stream));
+  return CLASFV_OK;
+}
+
 int clasfv_preprocess_video(const uint8_t* frames, int T, int Hs, int Ws, int H, int W, float* out, void* stream) {
   if (!frames || !out || T < 1 || Hs < 1 || Ws < 1 || H < 1 || W < 1 || H > 65535 || T > 65535)
     return fail(CLASFV_EINVAL, "bad argument");

@@ -17,3 +17,5 @@ hipError_t launch_zeroone_normalize(float* v, int64_t n, float* part, hipStream_
 int zeroone_partials_floats();
 hipError_t launch_preprocess_video(const uint8_t* frames, int T, int Hs, int Ws, int H, int W, float* out,
                                    hipStream_t s);
+hipError_t launch_warp_backward(const float* gout, const float* img, int N, int C, int H, int W, const float* motion,
+                                int64_t m_sn, int64_t m_sc, float* gimg, float* gmot, hipStream_t s);

@@ -4,6 +4,7 @@
 //   pass_labels        softmax -> temporal resample -> argmax   src/fuse_utils.py:53-80
 //   fuse_votes         per-frame label fusion            src/fuse_utils.py:82-100
 //   warp               generate_2dmotion_field + grid_sample   src/transform_utils.py:14-34
+//   warp_backward      its gradients (autograd of the training losses, src/clasfv_losses.py:29-136)
 //   zeroone_normalize  zeroone_normalizer                src/echonet_dataset.py:38-50
 //   preprocess_video   frames -> (3,T,H,W) + trilinear resize   motion_segment.py:96-106
 //
@@ -279,6 +280,61 @@ __global__ void warp_kernel(const float* __restrict__ img, int N, int C, int H, 
   }
 }
 
+// Backward of warp_kernel (grid_sampler_2d_backward, bilinear, border, align_corners=False, as
+// PyTorch's vectorised CPU kernel): per output pixel and channel, grad_img gets gOut * corner
+// weight at the four corners (float atomics: the summation order differs from the CPU's sequential
+// scatter, so grad_img matches to rounding, not bit for bit); the motion gradient accumulates
+// fma(se_v - sw_v, n, (ne_v - nw_v) * s) * gOut (x) and fma(se_v - ne_v, w, (sw_v - nw_v) * e) * gOut
+// (y) over channels, times W/2 (H/2) when the unclipped source coordinate lies strictly inside
+// (0, W-1), else 0 (border clipping kills the gradient) -- bit-exact vs the CPU kernel.
+__global__ void warp_backward_kernel(const float* __restrict__ gout, const float* __restrict__ img, int N, int C, int H,
+                                     int W, const float* __restrict__ motion, int64_t m_sn, int64_t m_sc,
+                                     float* __restrict__ gimg, float* __restrict__ gmot) {
+  const size_t HW = (size_t)H * W;
+  const size_t total = (size_t)N * HW;
+  const float sx = (float)W * 0.5f, sy = (float)H * 0.5f;
+  for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < total; g += (size_t)gridDim.x * blockDim.x) {
+    const int n = (int)(g / HW);
+    const int pix = (int)(g - (size_t)n * HW);
+    const int i = pix / W, j = pix - (pix / W) * W;
+    const float* mp = motion + n * m_sn + pix;
+    const float gx = linspace_pm1(j, W) + mp[0];
+    const float gy = linspace_pm1(i, H) + mp[m_sc];
+    const float ux = fmaxf(fmaf(gx + 1.f, sx, -0.5f), 0.f), uy = fmaxf(fmaf(gy + 1.f, sy, -0.5f), 0.f);
+    const float ix = fminf(ux, (float)(W - 1)), iy = fminf(uy, (float)(H - 1));
+    const float mx = (ux != 0.f && ix != (float)(W - 1)) ? sx : 0.f;
+    const float my = (uy != 0.f && iy != (float)(H - 1)) ? sy : 0.f;
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const int x0 = (int)fx0, y0 = (int)fy0, x1 = x0 + 1, y1 = y0 + 1;
+    const float we = ix - fx0, ee = (fx0 + 1.f) - ix, wn = iy - fy0, ws = (fy0 + 1.f) - iy;
+    const float wnw = ws * ee, wne = ws * we, wsw = wn * ee, wse = wn * we;
+    const bool in_x1 = x1 < W, in_y1 = y1 < H;
+    float ax = 0.f, ay = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const size_t plane = ((size_t)n * C + c) * HW;
+      const float go = gout[plane + pix];
+      const float* src = img + plane;
+      const float vnw = src[y0 * W + x0];
+      const float vne = in_x1 ? src[y0 * W + x1] : 0.f;
+      const float vsw = in_y1 ? src[y1 * W + x0] : 0.f;
+      const float vse = (in_x1 && in_y1) ? src[y1 * W + x1] : 0.f;
+      if (gimg) {
+        float* d = gimg + plane;
+        atomicAdd(d + y0 * W + x0, go * wnw);
+        if (in_x1) atomicAdd(d + y0 * W + x1, go * wne);
+        if (in_y1) atomicAdd(d + y1 * W + x0, go * wsw);
+        if (in_x1 && in_y1) atomicAdd(d + y1 * W + x1, go * wse);
+      }
+      ax = fmaf(fmaf(vse - vsw, wn, (vne - vnw) * ws), go, ax);
+      ay = fmaf(fmaf(vse - vne, we, (vsw - vnw) * ee), go, ay);
+    }
+    if (gmot) {
+      gmot[(size_t)n * 2 * HW + pix] = ax * mx;
+      gmot[((size_t)n * 2 + 1) * HW + pix] = ay * my;
+    }
+  }
+}
+
 // ---- preprocess_video ---------------------------------------------------------------------------
 // motion_segment.py:96-106: (T,Hs,Ws,3) uint8 RGB frames -> (3,T,Hs,Ws) float32 -> F.interpolate(
 // size=(T,H,W), mode="trilinear", align_corners=True). T is unchanged, so the temporal weights are
@@ -409,6 +465,14 @@ hipError_t launch_warp(const float* img, int N, int C, int H, int W, const float
   const size_t total = (size_t)N * H * W;
   hipLaunchKernelGGL(warp_kernel, dim3(blocks_for(total, 256, 8192)), dim3(256), 0, s, img, N, C, H, W, motion, m_sn,
                      m_sc, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_warp_backward(const float* gout, const float* img, int N, int C, int H, int W, const float* motion,
+                                int64_t m_sn, int64_t m_sc, float* gimg, float* gmot, hipStream_t s) {
+  const size_t total = (size_t)N * H * W;
+  hipLaunchKernelGGL(warp_backward_kernel, dim3(blocks_for(total, 256, 8192)), dim3(256), 0, s, gout, img, N, C, H, W,
+                     motion, m_sn, m_sc, gimg, gmot);
   return hipGetLastError();
 }
 

@@ -38,7 +38,9 @@ __device__ inline int xcd_swizzle_w(int b, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
-template <int NT>
+// KO != 0 only in tools/convbench.hip (knock-out timing builds): bit 1 no transform, 2 no raw DMA,
+// 4 no U loads, 8 no epilogue, 16 no MFMA.
+template <int NT, int KO = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino(ConvParams p, int n_co,
                                                                                              int n_tiles) {
   __shared__ __align__(16) char smem[RAW_STAGES * RAW_BYTES + 2 * V_BYTES];
@@ -73,6 +75,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     d_off[j] = off;
   }
   auto issue_raw = [&](int chunk, int buf) {
+    if constexpr (KO & 2) return;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const void* src = (d_off[j] >= 0 && chunk >= 0) ? (const void*)(x + (size_t)d_off[j] + chunk * 8) : p.zero;
@@ -85,6 +88,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // ---- transform: thread = (tile tt, channel cc) of the chunk
   const int tt = tid >> 3, cc = tid & 7;
   auto transform = [&](int buf_raw, int buf_v) {
+    if constexpr (KO & 1) return;
     const float* rb = reinterpret_cast<const float*>(raw + buf_raw * RAW_BYTES) + tt * 128 + cc;
     float d[16];
 #pragma unroll
@@ -115,6 +119,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float* ub = U + (((size_t)wid * CO + n0 + l16) * 4 + q) * 8;
   f32x4 u0[NT][2], u1[NT][2], u2[NT][2];
   auto load_u = [&](int chunk, f32x4 (&u)[NT][2]) {
+    if constexpr (KO & 4) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) u[nt][0] = u[nt][1] = f32x4{1.f, 1.f, 1.f, 1.f} * (float)chunk;
+      return;
+    }
     const float* b = ub + (size_t)chunk * 4 * CO * 32;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -168,9 +177,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt)
-            acc[j][m][nt] =
-                __builtin_amdgcn_mfma_f32_16x16x4f32(a[2 * m + s], uc[nt][j >> 1][(j & 1) * 2 + s], acc[j][m][nt], 0, 0, 0);
+          for (int nt = 0; nt < NT; ++nt) {
+            if constexpr (KO & 16)
+              acc[j][m][nt][0] += a[2 * m + s] * uc[nt][j >> 1][(j & 1) * 2 + s];
+            else
+              acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2 * m + s], uc[nt][j >> 1][(j & 1) * 2 + s],
+                                                                   acc[j][m][nt], 0, 0, 0);
+          }
     }
   };
   // Full triples branch-free (keeps the compiler's own vmcnt bookkeeping exact), then the tail.
@@ -186,6 +199,52 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // ---- epilogue: Y = A^T M A. Wave i holds row i of M: the column combination (. A) is done in
   // registers, Z_i = (M_i0 + M_i1 + M_i2, M_i1 - M_i2 - M_i3); the row combination (A^T .) needs all
   // four waves and goes through LDS: Z[i][tile][co][2] (48 KB), one barrier.
+  if constexpr ((KO & 8) != 0) {
+    float sink = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) sink += acc[j][m][nt][0] + acc[j][m][nt][3];
+    if (sink == 1.2345f) reinterpret_cast<float*>(p.y)[tid] = sink;
+    return;
+  }
+  // Unit = (tile, 4 consecutive channels): 16-B bias / residual loads and 16-B stores. All of a
+  // thread's global loads are issued before the LDS exchange (their latency hides behind it, and
+  // res may alias y: no load can then wait behind a store).
+  constexpr int CQ = 4 * NT, UNITS = BT * CQ, UPT = (UNITS + 255) / 256;
+  const float* res = reinterpret_cast<const float*>(p.res);
+  float* yout = reinterpret_cast<float*>(p.y);
+  size_t u_o[UPT];
+  int u_ok[UPT], u_z[UPT];
+  f32x4 u_b[UPT], u_r[UPT][4];
+#pragma unroll
+  for (int u = 0; u < UPT; ++u) {
+    const int un = tid + 256 * u;
+    const int tl = un / CQ, cq = un - tl * CQ;
+    const int tg = t0 + tl;
+    const bool live = un < UNITS && tg < n_tiles;
+    const int tgc = live ? tg : t0;
+    const int f = tgc / (TY * TX), rem = tgc - f * (TY * TX);
+    const int ty = rem / TX, tx = rem - ty * TX;
+    const int co = n0 + 4 * cq;
+    u_o[u] = ((size_t)(f * H + 2 * ty) * W + 2 * tx) * CO + co;
+    u_z[u] = tl * (16 * NT) + 4 * cq;
+    int ok = 0;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        if (live && 2 * ty + a < H && 2 * tx + b < W) ok |= 1 << (2 * a + b);
+    u_ok[u] = ok;
+    u_b[u] = (p.bias && live) ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int px = 0; px < 4; ++px)
+      u_r[u][px] = (res && (ok >> px & 1))
+                       ? *reinterpret_cast<const f32x4*>(res + u_o[u] + (size_t)((px >> 1) * W + (px & 1)) * CO)
+                       : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   f32x2* zs = reinterpret_cast<f32x2*>(smem);
   __syncthreads();  // everyone is done with raw / V
 #pragma unroll
@@ -198,36 +257,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         zs[(wid * BT + m * 16 + 4 * q + r) * (16 * NT) + nt * 16 + l16] = f32x2{m0 + m1 + m2, m1 - m2 - m3};
       }
   __syncthreads();
-  constexpr int PAIRS = BT * 16 * NT;  // (tile, channel) pairs of the block
 #pragma unroll
-  for (int k2 = 0; k2 < PAIRS / 256; ++k2) {
-    const int pr = tid + 256 * k2;
-    const int tl = pr / (16 * NT), cl = pr - tl * (16 * NT);
-    const int tg = t0 + tl;
-    if (tg >= n_tiles) continue;
-    f32x2 z[4];
+  for (int u = 0; u < UPT; ++u) {
+    if (!u_ok[u]) continue;
+    // z[i][h]: channels 2h, 2h+1 of row i as {c.col0, c.col1, c'.col0, c'.col1}
+    f32x4 z[4][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) z[i] = zs[(i * BT + tl) * (16 * NT) + cl];
-    const int co = n0 + cl;
-    const float bv = p.bias ? p.bias[co] : 0.f;
-    const int f = tg / (TY * TX), rem = tg - f * (TY * TX);
-    const int ty = rem / TX, tx = rem - ty * TX;
+    for (int i = 0; i < 4; ++i) {
+      const f32x4* zp = reinterpret_cast<const f32x4*>(zs + i * BT * (16 * NT) + u_z[u]);
+      z[i][0] = zp[0];
+      z[i][1] = zp[1];
+    }
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      const int yy = 2 * ty + a;
-      if (yy >= H) continue;
-      const f32x2 y = a == 0 ? z[0] + z[1] + z[2] : z[1] - z[2] - z[3];
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        const int xx = 2 * tx + b;
-        if (xx >= W) continue;
-        const size_t o = ((size_t)(f * H + yy) * W + xx) * CO + co;
-        float v = y[b] + bv;
-        if (p.res) v += reinterpret_cast<const float*>(p.res)[o];
-        if (p.relu) v = fmaxf(v, 0.f);
-        reinterpret_cast<float*>(p.y)[o] = v;
+        const int px = 2 * a + b;
+        if (!(u_ok[u] >> px & 1)) continue;
+        f32x4 v;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int h = c >> 1, e = (c & 1) * 2 + b;
+          const float y = a == 0 ? z[0][h][e] + z[1][h][e] + z[2][h][e] : z[1][h][e] - z[2][h][e] - z[3][h][e];
+          float o = y + u_b[u][c];
+          if (res) o += u_r[u][px][c];
+          if (p.relu) o = fmaxf(o, 0.f);
+          v[c] = o;
+        }
+        *reinterpret_cast<f32x4*>(yout + u_o[u] + (size_t)(a * W + b) * CO) = v;
       }
-    }
   }
 }
 
@@ -249,6 +307,27 @@ hipError_t launch_wino(const ConvParams& p, hipStream_t s) {
   hipLaunchKernelGGL((conv_wino<3>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles);
   return hipGetLastError();
 }
+
+#ifdef CLASFV_KNOCKOUTS
+hipError_t launch_wino_ko(const ConvParams& p, hipStream_t s, int ko) {
+  const int n_tiles = p.N * p.To * ((p.Ho + 1) / 2) * ((p.Wo + 1) / 2);
+  const int n_co = p.Cout / 48;
+  const dim3 g(((n_tiles + BT - 1) / BT) * n_co);
+  switch (ko) {
+    case 0: hipLaunchKernelGGL((conv_wino<3, 0>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 1: hipLaunchKernelGGL((conv_wino<3, 1>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 2: hipLaunchKernelGGL((conv_wino<3, 2>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 4: hipLaunchKernelGGL((conv_wino<3, 4>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 8: hipLaunchKernelGGL((conv_wino<3, 8>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 16: hipLaunchKernelGGL((conv_wino<3, 16>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 7: hipLaunchKernelGGL((conv_wino<3, 7>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 15: hipLaunchKernelGGL((conv_wino<3, 15>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 6: hipLaunchKernelGGL((conv_wino<3, 6>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+#endif
 
 // Host: U[c/8][i][o][(c%8)/2][j][c%2] = (G g_{o,c} G^T)[i][j] in double, g = folded 3x3 kernel.
 void wino_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U) {

@@ -110,6 +110,15 @@ int clasfv_fuse_votes(const uint8_t* labels_dev, int K, int T, int step, int H, 
 int clasfv_warp(const float* img_dev, int N, int C, int H, int W, const float* motion_dev, int64_t m_sn,
                 int64_t m_sc, float* out_dev, void* stream);
 
+/* Gradients of clasfv_warp (training losses, src/clasfv_losses.py:29-136, backpropagate through it):
+ * grad_img_dev (N,C,H,W) += d loss / d img (atomically accumulated: zero it first; may be NULL),
+ * grad_motion_dev (N,2,H,W) dense = d loss / d motion (may be NULL), from grad_out_dev (N,C,H,W).
+ * grad_motion is bit-exact vs PyTorch's CPU grid_sample backward; grad_img matches it to float
+ * rounding (different summation order). motion strides as in clasfv_warp. */
+int clasfv_warp_backward(const float* grad_out_dev, const float* img_dev, int N, int C, int H, int W,
+                         const float* motion_dev, int64_t m_sn, int64_t m_sc, float* grad_img_dev,
+                         float* grad_motion_dev, void* stream);
+
 /* ---- preprocessing (motion_segment.py:96-106, src/echonet_dataset.py:38-50) --------------------- */
 /* frames_dev (T,Hs,Ws,3) uint8 RGB -> out_dev (3,T,H,W) float32, resized as
  * F.interpolate(size=(T,H,W), mode="trilinear", align_corners=True) on the (1,3,T,Hs,Ws) float

@@ -212,6 +212,64 @@ def test_warp_vs_reference_golden():
     np.testing.assert_array_equal(box, g["box_zero"])
 
 
+def test_warp_backward_vs_reference_golden():
+    """clasfv_warp_backward: motion gradient bit-exact vs the reference's CPU grid_sample backward,
+    image gradient to float rounding (atomic scatter order)."""
+    from clasfv_amd.warp import warp
+    from tests.golden.make_golden_losses import loss_inputs
+    d, g = loss_inputs(), golden("losses.npz")
+    img = torch.from_numpy(d["warp_img"]).cuda().requires_grad_()
+    mot = torch.from_numpy(d["warp_motion"]).cuda().requires_grad_()
+    out = warp(img, mot)
+    out.backward(torch.from_numpy(d["warp_gout"]).cuda())
+    np.testing.assert_array_equal(out.detach().cpu().numpy(), g["warp_out"])
+    np.testing.assert_array_equal(mot.grad.cpu().numpy(), g["warp_grad_motion"])
+    np.testing.assert_allclose(img.grad.cpu().numpy(), g["warp_grad_img"], rtol=1e-5, atol=1e-6)
+
+
+def test_warp_backward_strided_motion_vs_oracle():
+    from clasfv_amd.warp import warp
+    rng = np.random.default_rng(5)
+    img = rng.uniform(0, 1, (2, 2, 24, 36)).astype(np.float32)
+    motion = np.tanh(rng.normal(0, 0.4, (2, 4, 3, 24, 36))).astype(np.float32)  # large: exercises clipping
+    gout = rng.normal(0, 1, (2, 2, 24, 36)).astype(np.float32)
+    mg = torch.from_numpy(motion).cuda().requires_grad_()
+    ig = torch.from_numpy(img).cuda().requires_grad_()
+    warp(ig, mg[:, 2:, 1]).backward(torch.from_numpy(gout).cuda())
+    mc = torch.from_numpy(motion).requires_grad_()
+    ic = torch.from_numpy(img).requires_grad_()
+    warp_ref.warp(ic, mc[:, 2:, 1]).backward(torch.from_numpy(gout))
+    np.testing.assert_array_equal(mg.grad.cpu().numpy(), mc.grad.numpy())
+    np.testing.assert_allclose(ig.grad.cpu().numpy(), ic.grad.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_training_losses_vs_reference_golden():
+    """deformation_motion_loss (OTA) and motion_seg_loss (SGS/OTS) through the HIP warp: loss values
+    and autograd gradients vs the reference's CPU run (fp32; gradients summed over many warps, so
+    compared to float rounding)."""
+    import torch.nn.functional as F
+    from clasfv_amd import losses as L
+    from tests.golden.make_golden_losses import loss_inputs
+    d, g = loss_inputs(), golden("losses.npz")
+    video = torch.from_numpy(d["video"]).cuda().requires_grad_()
+    motion = torch.from_numpy(d["motion"]).cuda().requires_grad_()
+    loss = L.deformation_motion_loss(video, motion)
+    loss.backward()
+    np.testing.assert_allclose(loss.item(), g["ota_loss"], rtol=1e-5)  # GPU vs CPU reduction order
+    np.testing.assert_allclose(video.grad.cpu().numpy(), g["ota_grad_video"], rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(motion.grad.cpu().numpy(), g["ota_grad_motion"], rtol=1e-4, atol=1e-7)
+
+    motion = torch.from_numpy(d["motion"]).cuda().requires_grad_()
+    logits = torch.from_numpy(d["logits"]).cuda().requires_grad_()
+    flow, ots = L.motion_seg_loss(d["ed"], d["es"], d["ed_index"], d["es_index"], motion, F.softmax(logits, dim=1),
+                                  start=0, end=d["video"].shape[2])
+    (flow + ots).backward()
+    np.testing.assert_allclose(flow.item(), g["sgs_flow_loss"], rtol=1e-5)
+    np.testing.assert_allclose(ots.item(), g["sgs_ots_loss"], rtol=1e-5)
+    np.testing.assert_allclose(motion.grad.cpu().numpy(), g["sgs_grad_motion"], rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(logits.grad.cpu().numpy(), g["sgs_grad_logits"], rtol=1e-4, atol=1e-7)
+
+
 def test_warp_strided_motion_slice_vs_oracle():
     from clasfv_amd.warp import warp
     rng = np.random.default_rng(3)

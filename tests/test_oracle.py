@@ -165,3 +165,16 @@ def test_preprocess_oracle_bitexact_vs_torch(shape):
     ref = F.interpolate(torch.from_numpy(v.transpose(3, 0, 1, 2).astype(np.float32))[None], size=(T, H, W),
                         mode="trilinear", align_corners=True)[0].numpy()
     np.testing.assert_array_equal(fuse_ref.preprocess_frames(v, H, W), ref)
+
+
+def test_warp_backward_oracle_matches_reference():
+    """torch-CPU grid_sample autograd (the oracle for clasfv_warp_backward) vs the reference golden."""
+    from tests.golden.make_golden_losses import loss_inputs
+    d, g = loss_inputs(), golden("losses.npz")
+    img = torch.from_numpy(d["warp_img"]).requires_grad_()
+    mot = torch.from_numpy(d["warp_motion"]).requires_grad_()
+    out = warp_ref.warp(img, mot)
+    out.backward(torch.from_numpy(d["warp_gout"]))
+    np.testing.assert_array_equal(out.detach().numpy(), g["warp_out"])
+    np.testing.assert_array_equal(mot.grad.numpy(), g["warp_grad_motion"])
+    np.testing.assert_array_equal(img.grad.numpy(), g["warp_grad_img"])

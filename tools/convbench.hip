@@ -1,0 +1,104 @@
+// Stand-alone timing of one conv layer shape through the engine's kernels (not part of the product).
+// Build + run (GPU box): bash tools/convbench.sh
+//   convbench KIND N T H W CIN COUT [ITERS] [KO...]
+//   KIND: wino (1x3x3 s1), winot (3x1x1 s1), sp (1x3x3 direct), tp (3x1x1 direct), pw (1x1x1)
+// KO = knock-out variant of the Winograd kernels (see winograd.hip): timing only, results are wrong.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../fully-automated-multi-heartbeat-echocardiography-video-segmentation-and-motion-tracking_amd/csrc/common.h"
+
+hipError_t launch_wino_ko(const ConvParams& p, hipStream_t s, int ko);
+hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko);
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+static void* dev_random(size_t n, float lo, float hi, unsigned seed) {
+  std::vector<float> h(n);
+  unsigned s = seed * 2654435761u + 1;
+  for (size_t i = 0; i < n; ++i) {
+    s = s * 1664525u + 1013904223u;
+    h[i] = lo + (hi - lo) * ((s >> 8) * (1.0f / 16777216.0f));
+  }
+  void* d;
+  CK(hipMalloc(&d, n * 4));
+  CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+  return d;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 8) {
+    fprintf(stderr, "usage: convbench KIND N T H W CIN COUT [ITERS] [KO...]\n");
+    return 2;
+  }
+  const char* kind = argv[1];
+  const int N = atoi(argv[2]), T = atoi(argv[3]), H = atoi(argv[4]), W = atoi(argv[5]);
+  const int Cin = atoi(argv[6]), Cout = atoi(argv[7]);
+  const int iters = argc > 8 ? atoi(argv[8]) : 20;
+  std::vector<int> kos;
+  for (int i = 9; i < argc; ++i) kos.push_back(atoi(argv[i]));
+  if (kos.empty()) kos.push_back(0);
+  const bool wino = !strcmp(kind, "wino"), winot = !strcmp(kind, "winot");
+  const bool sp = wino || !strcmp(kind, "sp"), tp = winot || !strcmp(kind, "tp");
+  ConvParams p;
+  memset(&p, 0, sizeof(p));
+  p.N = N, p.Ti = T, p.Hi = H, p.Wi = W, p.Cin = Cin;
+  p.To = T, p.Ho = H, p.Wo = W, p.Cout = Cout;
+  p.KT = tp ? 3 : 1, p.KH = sp ? 3 : 1, p.KW = sp ? 3 : 1;
+  p.st = p.sh = p.sw = 1;
+  p.pt = tp ? 1 : 0, p.ph = sp ? 1 : 0, p.pw = sp ? 1 : 0;
+  p.K = p.KT * p.KH * p.KW * Cin;
+  p.Kp = (p.K + 15) / 16 * 16;
+  p.M = N * T * H * W;
+  p.relu = 1;
+  const size_t nx = (size_t)p.M * Cin, ny = (size_t)p.M * Cout;
+  p.x = dev_random(nx, 0.f, 1.f, 1);
+  const size_t nw = wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
+  p.w = dev_random(nw, -0.05f, 0.05f, 2);
+  p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
+  p.res = getenv("CB_NORES") ? nullptr : dev_random(ny, 0.f, 1.f, 4);
+  CK(hipMalloc(&p.y, ny * 4));
+  void* z;
+  CK(hipMalloc(&z, 256));
+  CK(hipMemset(z, 0, 256));
+  p.zero = z;
+  const double gflop = 2.0 * p.M * (double)Cout * Cin * p.KT * p.KH * p.KW * 1e-9;
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int ko : kos) {
+    auto launch = [&]() {
+      if (wino) CK(launch_wino_ko(p, s, ko));
+      else if (winot) CK(launch_winot_ko(p, s, ko));
+      else {
+        int mt, bn;
+        conv_pick_tile(p.M, Cout, 0, &mt, &bn);
+        CK(launch_conv(p, mt, bn, s));
+      }
+    };
+    for (int i = 0; i < 3; ++i) launch();
+    CK(hipEventRecord(a, s));
+    for (int i = 0; i < iters; ++i) launch();
+    CK(hipEventRecord(b, s));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ms /= iters;
+    printf("%s%-6s N=%d T=%d H=%d W=%d Cin=%d Cout=%d ko=%-2d  %8.3f ms  %7.1f TF(alg)\n", p.res ? "res   " : "nores ",
+           kind, N, T, H, W, Cin, Cout, ko, ms, gflop / ms);
+  }
+  return 0;
+}
