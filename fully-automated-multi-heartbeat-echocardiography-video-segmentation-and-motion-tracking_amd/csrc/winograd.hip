@@ -40,7 +40,10 @@ __device__ inline int xcd_swizzle_w(int b, int nb) {
 
 // KO != 0 only in tools/convbench.hip (knock-out timing builds): bit 1 no transform, 2 no raw DMA,
 // 4 no U loads, 8 no epilogue, 16 no MFMA.
-template <int NT, int KO = 0>
+// NCH > 0: the chunk count Cin/8 as a compile-time constant -> the chunk loop is fully unrolled and
+// the compiler's own vmcnt waits are exact (the runtime loop makes it wait for the previous chunk's
+// fetches too, one chunk early).
+template <int NT, int KO = 0, int NCH = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino(ConvParams p, int n_co,
                                                                                              int n_tiles) {
   __shared__ __align__(16) char smem[RAW_STAGES * RAW_BYTES + 2 * V_BYTES];
@@ -56,7 +59,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int t0 = (blk / n_co) * BT, n0 = (blk % n_co) * 16 * NT;
   const int H = p.Ho, W = p.Wo, C = p.Cin, CO = p.Cout;
   const int TY = (H + 1) >> 1, TX = (W + 1) >> 1;
-  const int nchunk = C >> 3;
+  const int nchunk = NCH > 0 ? NCH : C >> 3;
 
   // ---- per-lane DMA sources: instruction j of this wave fills 16-B slot s = (wid + 4j)*64 + lane
   int d_off[4];  // float offset of channel 0 of the source pixel, or -1 (zero padding)
@@ -87,12 +90,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
   // ---- transform: thread = (tile tt, channel cc) of the chunk
   const int tt = tid >> 3, cc = tid & 7;
-  auto transform = [&](int buf_raw, int buf_v) {
-    if constexpr (KO & 1) return;
+  // The transform is split so that the raw reads of chunk k+1 are issued before the MFMAs of chunk
+  // k and its arithmetic + V stores fill their issue gaps (sched_group_barrier in step()).
+  auto transform_read = [&](int buf_raw, float (&d)[16]) {
+    if constexpr (KO & 1) {
+#pragma unroll
+      for (int i2 = 0; i2 < 16; ++i2) d[i2] = (float)(buf_raw + i2);
+      return;
+    }
     const float* rb = reinterpret_cast<const float*>(raw + buf_raw * RAW_BYTES) + tt * 128 + cc;
-    float d[16];
 #pragma unroll
     for (int px = 0; px < 16; ++px) d[px] = rb[(px ^ (tt & 7)) * 8];
+  };
+  auto transform_write = [&](const float (&d)[16], int buf_v) {
+    if constexpr (KO & 1) return;
     float t[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {  // B^T d
@@ -152,7 +163,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __builtin_amdgcn_s_waitcnt(0x0F70 | (20 & 15) | ((20 >> 4) << 14));  // vmcnt(20): raw(0) landed
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
-  transform(0, 0);
+  {
+    float d[16];
+    transform_read(0, d);
+    transform_write(d, 0);
+  }
 
   const int a_off = (l16 * 4 + q) * 16;  // byte offset of the lane's 4 V values inside one e slice
   // One chunk k: U(k) is in `uc`, U(k+2) is fetched into `un` (3-way rotation, no register copies);
@@ -167,11 +182,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     issue_raw(k + 3 < nchunk ? k + 3 : -1, k % RAW_STAGES);
     load_u(k + 2 < nchunk ? k + 2 : 0, un);
     __builtin_amdgcn_sched_barrier(0);
-    if (k + 1 < nchunk) transform((k + 1) % RAW_STAGES, (k + 1) & 1);
     const char* vb = vbuf + (k & 1) * V_BYTES + a_off;
+    f32x4 a[4];  // {m0 s0, m0 s1, m1 s0, m1 s1} per j
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(vb + (4 * wid + j) * (BT * 32));  // {m0 s0, m0 s1, m1 s0, m1 s1}
+    for (int j = 0; j < 4; ++j) a[j] = *reinterpret_cast<const f32x4*>(vb + (4 * wid + j) * (BT * 32));
+    // transform raw(k+1) -> V[(k+1)&1] (on the last chunk it transforms the ring's past-the-end
+    // fetch into the V buffer nobody reads again: branch-free keeps one scheduling region)
+    float d[16];
+    transform_read((k + 1) % RAW_STAGES, d);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -179,22 +199,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) {
             if constexpr (KO & 16)
-              acc[j][m][nt][0] += a[2 * m + s] * uc[nt][j >> 1][(j & 1) * 2 + s];
+              acc[j][m][nt][0] += a[j][2 * m + s] * uc[nt][j >> 1][(j & 1) * 2 + s];
             else
-              acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2 * m + s], uc[nt][j >> 1][(j & 1) * 2 + s],
+              acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][2 * m + s], uc[nt][j >> 1][(j & 1) * 2 + s],
                                                                    acc[j][m][nt], 0, 0, 0);
           }
+    transform_write(d, (k + 1) & 1);
+    if constexpr (KO == 0) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+      }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
     }
   };
-  // Full triples branch-free (keeps the compiler's own vmcnt bookkeeping exact), then the tail.
-  int k = 0;
-  for (; k + 3 <= nchunk; k += 3) {
-    step(k, u0, u2);
-    step(k + 1, u1, u0);
-    step(k + 2, u2, u1);
+  if constexpr (NCH > 0) {
+#pragma unroll
+    for (int kk = 0; kk < NCH; kk += 3) {
+      step(kk, u0, u2);
+      if (kk + 1 < NCH) step(kk + 1, u1, u0);
+      if (kk + 2 < NCH) step(kk + 2, u2, u1);
+    }
+  } else {
+    // Full triples branch-free, then the tail.
+    int k = 0;
+    for (; k + 3 <= nchunk; k += 3) {
+      step(k, u0, u2);
+      step(k + 1, u1, u0);
+      step(k + 2, u2, u1);
+    }
+    if (k < nchunk) step(k, u0, u2);
+    if (k + 1 < nchunk) step(k + 1, u1, u0);
   }
-  if (k < nchunk) step(k, u0, u2);
-  if (k + 1 < nchunk) step(k + 1, u1, u0);
 
   // ---- epilogue: Y = A^T M A. Wave i holds row i of M: the column combination (. A) is done in
   // registers, Z_i = (M_i0 + M_i1 + M_i2, M_i1 - M_i2 - M_i3); the row combination (A^T .) needs all
@@ -304,7 +346,11 @@ hipError_t launch_wino(const ConvParams& p, hipStream_t s) {
   const int n_tiles = p.N * p.To * ((p.Ho + 1) / 2) * ((p.Wo + 1) / 2);
   const int n_co = p.Cout / 48;
   const int nb = (n_tiles + BT - 1) / BT;
-  hipLaunchKernelGGL((conv_wino<3>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles);
+  switch (p.Cin >> 3) {  // fully unrolled chunk loops for the layer1 / layer2 widths
+    case 8: hipLaunchKernelGGL((conv_wino<3, 0, 8>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 16: hipLaunchKernelGGL((conv_wino<3, 0, 16>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
+    default: hipLaunchKernelGGL((conv_wino<3, 0, 0>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
+  }
   return hipGetLastError();
 }
 
@@ -314,7 +360,8 @@ hipError_t launch_wino_ko(const ConvParams& p, hipStream_t s, int ko) {
   const int n_co = p.Cout / 48;
   const dim3 g(((n_tiles + BT - 1) / BT) * n_co);
   switch (ko) {
-    case 0: hipLaunchKernelGGL((conv_wino<3, 0>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 0: return launch_wino(p, s);
+    case 100: hipLaunchKernelGGL((conv_wino<3, 0>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
     case 1: hipLaunchKernelGGL((conv_wino<3, 1>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
     case 2: hipLaunchKernelGGL((conv_wino<3, 2>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
     case 4: hipLaunchKernelGGL((conv_wino<3, 4>), g, dim3(256), 0, s, p, n_co, n_tiles); break;

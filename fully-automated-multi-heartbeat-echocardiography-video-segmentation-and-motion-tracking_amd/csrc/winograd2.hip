@@ -1,0 +1,342 @@
+// Patch-tiled fused Winograd F(2x2, 3x3) for the widest stride-1 1x3x3 fp32 convs (R(2+1)D-18 layer1
+// at 32x112x112 clips: 56x56 feature maps; also layer2 of 224x224 clips). Same op, arithmetic and U
+// layout as conv_wino (winograd.hip) -- M_e = sum_ci V_e U_e on exact-fp32 v_mfma_f32_16x16x4_f32,
+// Y = A^T M A -- with two changes that matter on MI355X:
+//  * the 4x4 input windows of a block's tiles are fetched as whole 10x10-pixel patches (a patch =
+//    4x4 tiles = 8x8 output pixels): 400 16-B LDS-DMA slots per 8-channel chunk for 32 tiles
+//    instead of 32 x 16 pixels = 1024 (2.56x fewer raw bytes through L2 and the TA);
+//  * the transform of chunk k+1 is split around the MFMAs of chunk k: its LDS reads are issued
+//    before them and its arithmetic and V stores are placed in the MFMA issue gaps
+//    (sched_group_barrier), so the matrix pipe no longer idles while a wave transforms.
+// Layer1 (30 clips, 64->144): 2.89 -> 2.61 ms (tools/convbench.sh). Requires Ho, Wo % 8 == 0.
+#include "common.h"
+
+namespace {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+
+__device__ inline int xcd_swizzle_p(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+__device__ inline void dma16(const void* src, void* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+// conv_wino_q: block = 4 waves (wave = transform row i) x 2 patches (32 tiles) x 48 output channels,
+// 2 blocks per CU (56 KB LDS); U operands in registers, fetched two chunks ahead (3-way rotation);
+// raw ring 3 x 8 KB, V double-buffered; one barrier per chunk.
+constexpr int Q_BT = 32;
+constexpr int Q_RAW = 8 * 1024;       // 8 DMA wave-instructions (400 slots used)
+constexpr int Q_V = 16 * Q_BT * 32;   // 16 KB
+constexpr int Q_LDS = 3 * Q_RAW + 2 * Q_V;
+
+template <int NCH, int KO = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino_q(ConvParams p, int n_co,
+                                                                                             int n_patches) {
+  __shared__ __align__(16) char smem[Q_LDS];
+  char* raw = smem;
+  char* vbuf = smem + 3 * Q_RAW;
+
+  const float* x = reinterpret_cast<const float*>(p.x);
+  const float* U = reinterpret_cast<const float*>(p.w);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, l16 = lane & 15;
+  const int blk = xcd_swizzle_p(blockIdx.x, gridDim.x);
+  const int pg0 = (blk / n_co) * 2, n0 = (blk % n_co) * 48;
+  const int H = p.Ho, W = p.Wo, C = p.Cin, CO = p.Cout;
+  const int PY = H >> 3, PX = W >> 3;
+  const int nchunk = NCH > 0 ? NCH : C >> 3;
+
+  // raw DMA: instruction j of this wave fills slots s = (wid + 4j)*64 + lane, s = pp*200 + pix*2 + half
+  int d_off[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int s = (wid + 4 * j) * 64 + lane;
+    int off = -1;
+    if (s < 400) {
+      const int pp = s / 200, rem = s - pp * 200, pix = rem >> 1, half = rem & 1;
+      const int py = pix / 10, px = pix - py * 10;
+      const int gp = pg0 + pp;
+      if (gp < n_patches) {
+        const int f = gp / (PY * PX), r = gp - f * (PY * PX);
+        const int pr = r / PX, pc = r - pr * PX;
+        const int yy = pr * 8 - 1 + py, xx = pc * 8 - 1 + px;
+        if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) off = ((f * H + yy) * W + xx) * C + half * 4;
+      }
+    }
+    d_off[j] = off;
+  }
+  auto issue_raw = [&](int k, int stage) __attribute__((always_inline)) {
+    if constexpr (KO & 2) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const void* src = (k < nchunk && d_off[j] >= 0) ? (const void*)(x + (size_t)d_off[j] + k * 8) : p.zero;
+      dma16(src, raw + stage * Q_RAW + (wid + 4 * j) * 1024);
+    }
+  };
+  // U: lane (co = l16, q) of wave (e row) wid, n tile nt: 8 floats U[chunk][wid][co][q][j][s]
+  const float* ub = U + (((size_t)wid * CO + n0 + l16) * 4 + q) * 8;
+  auto load_u = [&](int k, f32x4 (&u)[3][2]) __attribute__((always_inline)) {
+    if constexpr (KO & 4) {
+#pragma unroll
+      for (int nt = 0; nt < 3; ++nt) u[nt][0] = u[nt][1] = f32x4{1.f, 1.f, 1.f, 1.f} * (float)k;
+      return;
+    }
+    const float* b = ub + (size_t)(k < nchunk ? k : 0) * 4 * CO * 32;
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) u[nt][h] = *reinterpret_cast<const f32x4*>(b + (size_t)nt * 16 * 32 + h * 4);
+  };
+  // transform thread = (tile tt = pp*16 + ly*4 + lx, channel cc)
+  const int tt = tid >> 3, cc = tid & 7;
+  const int raw_off = (tt >> 4) * 800 + (2 * ((tt >> 2) & 3) * 10 + 2 * (tt & 3)) * 8 + cc;
+  const int v_off = (((tt & 15) * 4 + (cc >> 1)) * 2 + (tt >> 4)) * 2 + (cc & 1);  // V[e][tile&15][ci>>1][pp][ci&1]
+  auto transform_read = [&](int rstage, float (&d)[16]) __attribute__((always_inline)) {
+    if constexpr (KO & 1) {
+#pragma unroll
+      for (int i2 = 0; i2 < 16; ++i2) d[i2] = (float)(rstage + i2);
+      return;
+    }
+    const float* rb = reinterpret_cast<const float*>(raw + rstage * Q_RAW) + raw_off;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) d[4 * r + c] = rb[(r * 10 + c) * 8];
+  };
+  auto transform_write = [&](const float (&d)[16], int vstage) __attribute__((always_inline)) {
+    if constexpr (KO & 1) return;
+    float t[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      t[0 * 4 + c] = d[0 * 4 + c] - d[2 * 4 + c];
+      t[1 * 4 + c] = d[1 * 4 + c] + d[2 * 4 + c];
+      t[2 * 4 + c] = d[2 * 4 + c] - d[1 * 4 + c];
+      t[3 * 4 + c] = d[1 * 4 + c] - d[3 * 4 + c];
+    }
+    float* vb = reinterpret_cast<float*>(vbuf + vstage * Q_V) + v_off;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      vb[(4 * r + 0) * Q_BT * 8] = t[4 * r + 0] - t[4 * r + 2];
+      vb[(4 * r + 1) * Q_BT * 8] = t[4 * r + 1] + t[4 * r + 2];
+      vb[(4 * r + 2) * Q_BT * 8] = t[4 * r + 2] - t[4 * r + 1];
+      vb[(4 * r + 3) * Q_BT * 8] = t[4 * r + 1] - t[4 * r + 3];
+    }
+  };
+
+  f32x4 u0[3][2], u1[3][2], u2[3][2];
+  f32x4 acc[4][2][3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int nt = 0; nt < 3; ++nt) acc[j][m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: raw(0), U(0), raw(1), U(1), raw(2); transform(0). Per chunk each wave issues exactly
+  // 2 DMAs + 6 U loads (past-the-end fetches read the zero block / chunk 0), so the counts are exact.
+  issue_raw(0, 0);
+  load_u(0, u0);
+  issue_raw(1, 1);
+  load_u(1, u1);
+  issue_raw(2, 2);
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (16 & 15) | ((16 >> 4) << 14));  // vmcnt(16): raw(0) landed
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    float d[16];
+    transform_read(0, d);
+    transform_write(d, 0);
+  }
+
+  const int a_off = (l16 * 4 + q) * 16;
+  auto step = [&](int k, f32x4 (&uc)[3][2], f32x4 (&un)[3][2]) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_waitcnt(0x0F70 | 8);  // vmcnt(8): raw(k+1), U(k) landed
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    issue_raw(k + 3, k % 3);
+    load_u(k + 2, un);
+    __builtin_amdgcn_sched_barrier(0);
+    const char* vb = vbuf + (k & 1) * Q_V + a_off;
+    f32x4 a[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = *reinterpret_cast<const f32x4*>(vb + (4 * wid + j) * (Q_BT * 32));
+    float d[16];  // raw(k+1) -> V((k+1)&1); branch-free (the last chunk transforms the unused fetch)
+    transform_read((k + 1) % 3, d);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int nt = 0; nt < 3; ++nt) {
+            if constexpr (KO & 16)
+              acc[j][m][nt][0] += a[j][2 * m + s2] * uc[nt][j >> 1][(j & 1) * 2 + s2];
+            else
+              acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][2 * m + s2], uc[nt][j >> 1][(j & 1) * 2 + s2],
+                                                                   acc[j][m][nt], 0, 0, 0);
+          }
+    transform_write(d, (k + 1) & 1);
+    if constexpr (KO == 0) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+      }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+    }
+  };
+  if constexpr (NCH > 0) {
+#pragma unroll
+    for (int kk = 0; kk < NCH; kk += 3) {
+      step(kk, u0, u2);
+      if (kk + 1 < NCH) step(kk + 1, u1, u0);
+      if (kk + 2 < NCH) step(kk + 2, u2, u1);
+    }
+  } else {
+    int k = 0;
+    for (; k + 3 <= nchunk; k += 3) {
+      step(k, u0, u2);
+      step(k + 1, u1, u0);
+      step(k + 2, u2, u1);
+    }
+    if (k < nchunk) step(k, u0, u2);
+    if (k + 1 < nchunk) step(k + 1, u1, u0);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // drain past-the-end fetches before LDS is reused
+
+  if constexpr ((KO & 8) != 0) {
+    float sink = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int nt = 0; nt < 3; ++nt) sink += acc[j][m][nt][0] + acc[j][m][nt][3];
+    if (sink == 1.2345f) reinterpret_cast<float*>(p.y)[tid] = sink;
+    return;
+  }
+  // epilogue: unit = (tile, 4 channels); Z[i][tile][co] f32x2 (48 KB) through LDS
+  constexpr int CQ = 12, UNITS = Q_BT * CQ, UPT = (UNITS + 255) / 256;
+  const float* res = reinterpret_cast<const float*>(p.res);
+  float* yout = reinterpret_cast<float*>(p.y);
+  size_t u_o[UPT];
+  int u_ok[UPT], u_z[UPT];
+  f32x4 u_b[UPT], u_r[UPT][4];
+#pragma unroll
+  for (int u = 0; u < UPT; ++u) {
+    const int un = tid + 256 * u;
+    const int tl = un / CQ, cq = un - tl * CQ;
+    const int gp = pg0 + (tl >> 4);
+    const bool live = un < UNITS && gp < n_patches;
+    const int gpc = live ? gp : pg0;
+    const int f = gpc / (PY * PX), r = gpc - f * (PY * PX);
+    const int pr = r / PX, pc = r - pr * PX;
+    const int yy = pr * 8 + 2 * ((tl >> 2) & 3), xx = pc * 8 + 2 * (tl & 3);
+    const int co = n0 + 4 * cq;
+    u_o[u] = ((size_t)(f * H + yy) * W + xx) * CO + co;
+    u_z[u] = tl * 48 + 4 * cq;
+    u_ok[u] = live;
+    u_b[u] = (p.bias && live) ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int px = 0; px < 4; ++px)
+      u_r[u][px] = (res && live) ? *reinterpret_cast<const f32x4*>(res + u_o[u] + (size_t)((px >> 1) * W + (px & 1)) * CO)
+                                 : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  f32x2* zs = reinterpret_cast<f32x2*>(smem);
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float m0 = acc[0][m][nt][r], m1 = acc[1][m][nt][r], m2 = acc[2][m][nt][r], m3 = acc[3][m][nt][r];
+        zs[(wid * Q_BT + m * 16 + 4 * q + r) * 48 + nt * 16 + l16] = f32x2{m0 + m1 + m2, m1 - m2 - m3};
+      }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < UPT; ++u) {
+    if (!u_ok[u]) continue;
+    f32x4 z[4][2];
+#pragma unroll
+    for (int i2 = 0; i2 < 4; ++i2) {
+      const f32x4* zp = reinterpret_cast<const f32x4*>(zs + i2 * Q_BT * 48 + u_z[u]);
+      z[i2][0] = zp[0];
+      z[i2][1] = zp[1];
+    }
+#pragma unroll
+    for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+      for (int b2 = 0; b2 < 2; ++b2) {
+        f32x4 v;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int h = c >> 1, e = (c & 1) * 2 + b2;
+          const float y = a2 == 0 ? z[0][h][e] + z[1][h][e] + z[2][h][e] : z[1][h][e] - z[2][h][e] - z[3][h][e];
+          float o = y + u_b[u][c];
+          if (res) o += u_r[u][2 * a2 + b2][c];
+          if (p.relu) o = fmaxf(o, 0.f);
+          v[c] = o;
+        }
+        *reinterpret_cast<f32x4*>(yout + u_o[u] + (size_t)(a2 * W + b2) * CO) = v;
+      }
+  }
+}
+
+template <int NCH, int KO = 0>
+hipError_t launch_q(const ConvParams& p, hipStream_t s) {
+  const int n_patches = p.N * p.To * (p.Ho >> 3) * (p.Wo >> 3);
+  const int n_co = p.Cout / 48;
+  hipLaunchKernelGGL((conv_wino_q<NCH, KO>), dim3(((n_patches + 1) / 2) * n_co), dim3(256), 0, s, p, n_co, n_patches);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool winoq_supported(const ConvParams& p) {
+  return !p.in_bf16 && !p.out_bf16 && !p.stem && !p.x2 && p.KT == 1 && p.KH == 3 && p.KW == 3 && p.sh == 1 &&
+         p.sw == 1 && p.st == 1 && p.ph == 1 && p.pw == 1 && p.pt == 0 && p.Cin % 8 == 0 && p.Cout % 48 == 0 &&
+         p.Ho == p.Hi && p.Wo == p.Wi && p.To == p.Ti && p.Ho % 8 == 0 && p.Wo % 8 == 0 &&
+         (size_t)p.N * p.To * p.Ho * p.Wo * (p.Cin > p.Cout ? p.Cin : p.Cout) < ((size_t)1 << 31);
+}
+
+// p.w: conv_wino's U layout [Cin/8][4][Cout][4][4][2] (wino_transform_weights).
+hipError_t launch_winoq(const ConvParams& p, hipStream_t s) {
+  if (!winoq_supported(p)) return hipErrorInvalidValue;
+  switch (p.Cin >> 3) {
+    case 8: return launch_q<8>(p, s);
+    case 16: return launch_q<16>(p, s);
+    default: return launch_q<0>(p, s);
+  }
+}
+
+#ifdef CLASFV_KNOCKOUTS
+hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko) {
+  if (p.Cin != 64) return hipErrorInvalidValue;
+  switch (ko) {
+    case 0: return launch_q<8, 0>(p, s);
+    case 1: return launch_q<8, 1>(p, s);
+    case 2: return launch_q<8, 2>(p, s);
+    case 4: return launch_q<8, 4>(p, s);
+    case 6: return launch_q<8, 6>(p, s);
+    case 8: return launch_q<8, 8>(p, s);
+    case 15: return launch_q<8, 15>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+#endif

@@ -14,6 +14,7 @@
 
 hipError_t launch_wino_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko);
+hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko);
 
 #define CK(x)                                                                  \
   do {                                                                         \
@@ -49,7 +50,8 @@ int main(int argc, char** argv) {
   std::vector<int> kos;
   for (int i = 9; i < argc; ++i) kos.push_back(atoi(argv[i]));
   if (kos.empty()) kos.push_back(0);
-  const bool wino = !strcmp(kind, "wino"), winot = !strcmp(kind, "winot");
+  const bool winoq = !strcmp(kind, "winoq");
+  const bool wino = !strcmp(kind, "wino") || winoq, winot = !strcmp(kind, "winot");
   const bool sp = wino || !strcmp(kind, "sp"), tp = winot || !strcmp(kind, "tp");
   ConvParams p;
   memset(&p, 0, sizeof(p));
@@ -79,26 +81,33 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int ko : kos) {
-    auto launch = [&]() {
-      if (wino) CK(launch_wino_ko(p, s, ko));
-      else if (winot) CK(launch_winot_ko(p, s, ko));
-      else {
-        int mt, bn;
-        conv_pick_tile(p.M, Cout, 0, &mt, &bn);
-        CK(launch_conv(p, mt, bn, s));
-      }
-    };
-    for (int i = 0; i < 3; ++i) launch();
-    CK(hipEventRecord(a, s));
-    for (int i = 0; i < iters; ++i) launch();
-    CK(hipEventRecord(b, s));
-    CK(hipEventSynchronize(b));
-    float ms;
-    CK(hipEventElapsedTime(&ms, a, b));
-    ms /= iters;
-    printf("%s%-6s N=%d T=%d H=%d W=%d Cin=%d Cout=%d ko=%-2d  %8.3f ms  %7.1f TF(alg)\n", p.res ? "res   " : "nores ",
-           kind, N, T, H, W, Cin, Cout, ko, ms, gflop / ms);
-  }
+  auto launch = [&](int ko) {
+    if (winoq) CK(launch_winoq_ko(p, s, ko));
+    else if (wino) CK(launch_wino_ko(p, s, ko));
+    else if (winot) CK(launch_winot_ko(p, s, ko));
+    else {
+      int mt, bn;
+      conv_pick_tile(p.M, Cout, 0, &mt, &bn);
+      CK(launch_conv(p, mt, bn, s));
+    }
+  };
+  // warm every variant up (clocks settle), then interleave 3 timed rounds and keep each one's best
+  for (int ko : kos)
+    for (int i = 0; i < 10; ++i) launch(ko);
+  std::vector<float> best(kos.size(), 1e30f);
+  for (int rep = 0; rep < 3; ++rep)
+    for (size_t v = 0; v < kos.size(); ++v) {
+      CK(hipEventRecord(a, s));
+      for (int i = 0; i < iters; ++i) launch(kos[v]);
+      CK(hipEventRecord(b, s));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      ms /= iters;
+      if (ms < best[v]) best[v] = ms;
+    }
+  for (size_t v = 0; v < kos.size(); ++v)
+    printf("%s%-6s N=%d T=%d H=%d W=%d Cin=%d Cout=%d ko=%-3d  %8.3f ms  %7.1f TF(alg)\n", p.res ? "res   " : "nores ",
+           kind, N, T, H, W, Cin, Cout, kos[v], best[v], gflop / best[v]);
   return 0;
 }

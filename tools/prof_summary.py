@@ -12,7 +12,7 @@ import sys
 from collections import defaultdict
 
 
-KNOWN = ("conv_winot", "conv_wino", "conv_dma", "conv_stem_f32", "pack_input_kernel", "decoder_kernel",
+KNOWN = ("conv_winot", "conv_wino_q", "conv_wino", "conv_dma", "conv_stem_f32", "pack_input_kernel", "decoder_kernel",
          "preprocess_video_kernel")
 
 
