@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // while the MFMAs consume V[k&1].
   auto step = [&](int k, f32x4 (&uc)[NT][2], f32x4 (&un)[NT][2]) {
     // raw(k+1) and U(k) were issued two chunks ago; only chunk k-1's 10 fetches may be in flight.
-    __builtin_amdgcn_s_waitcnt(0x0F70 | 10);  // vmcnt(10)
+    __builtin_amdgcn_s_waitcnt(0x0070 | 10);  // vmcnt(10) lgkmcnt(0): own V stores done before the barrier
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);

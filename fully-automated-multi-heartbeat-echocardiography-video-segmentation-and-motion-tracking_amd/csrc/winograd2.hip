@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
   const int a_off = (l16 * 4 + q) * 16;
   auto step = [&](int k, f32x4 (&uc)[3][2], f32x4 (&un)[3][2]) __attribute__((always_inline)) {
-    __builtin_amdgcn_s_waitcnt(0x0F70 | 8);  // vmcnt(8): raw(k+1), U(k) landed
+    __builtin_amdgcn_s_waitcnt(0x0070 | 8);  // vmcnt(8): raw(k+1), U(k) landed; lgkmcnt(0): own V stores done
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
