@@ -313,7 +313,7 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   p.out_bf16 = c.out_bf16;
   if (c.dwino) {
     p.w = c.dwino;
-    static const bool no_patch = getenv("CLASFV_NO_WINO_PATCH") != nullptr;  // A/B switch
+    const bool no_patch = getenv("CLASFV_NO_WINO_PATCH") != nullptr;  // A/B switch (tests)
     if (!no_patch && winoq_supported(p)) {
       HIP_TRY(launch_winoq(p, s));
       *kname = "conv_wino_q";

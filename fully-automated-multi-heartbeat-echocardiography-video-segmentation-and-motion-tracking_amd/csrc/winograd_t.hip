@@ -533,7 +533,7 @@ bool winot_supported(const ConvParams& p) {
 // U: [Cin/8][6][Cout/64][64][8] transformed weights (winot_transform_weights).
 hipError_t launch_winot(const ConvParams& p, hipStream_t s) {
   if (!winot_supported(p)) return hipErrorInvalidValue;
-  static const bool no_t2 = getenv("CLASFV_NO_WINOT2") != nullptr;  // A/B switch
+  const bool no_t2 = getenv("CLASFV_NO_WINOT2") != nullptr;  // A/B switch (tests)
   // the 12-wave kernel wins from layer3 (490 blocks of 96 tiles) up; below one block per CU the
   // 2-blocks-per-CU 64-tile kernel keeps more of the chip busy
   if (!no_t2 && (size_t)p.N * (p.Ti / 4) * p.Hi * p.Wi / T2_BT * (p.Cout / 64) >= 256) return winot2_launch<0>(p, s);

@@ -427,3 +427,19 @@ def test_winograd_path_matches_direct_conv(model, monkeypatch, shape):
         import clasfv_amd.weights as W
         rs, rm = R.forward(W.synthetic_state_dict(W.DEFAULT_SEED), x.numpy())
         np.testing.assert_allclose(s_w.cpu().numpy(), rs.numpy(), rtol=0, atol=3e-3)
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112)])
+def test_kernel_variants_bitexact(model, monkeypatch, shape):
+    """The patch-tiled spatial Winograd kernel (conv_wino_q) and the 12-wave temporal one
+    (conv_winot2) compute the same products in the same accumulation order as conv_wino / conv_winot:
+    the forward must be bit-identical with them switched off."""
+    rng = np.random.default_rng(23)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    s_new, m_new = model(x)
+    monkeypatch.setenv("CLASFV_NO_WINO_PATCH", "1")
+    monkeypatch.setenv("CLASFV_NO_WINOT2", "1")
+    s_old, m_old = model(x)
+    monkeypatch.delenv("CLASFV_NO_WINO_PATCH")
+    monkeypatch.delenv("CLASFV_NO_WINOT2")
+    assert torch.equal(s_new, s_old) and torch.equal(m_new, m_old)
