@@ -19,7 +19,10 @@
 
 namespace {
 
-constexpr int PIX = 68;  // floats per staged pixel: 64 channels + 4 pad (fewer LDS bank conflicts)
+// floats per staged pixel: 64 channels + 8 pad. A ds_read_b128 lane group reads 8 distinct (source
+// pixel px, channel group q) slots at 16-B quad (px * PIX / 4 + q) mod 16 = (2 px + q) mod 16: all
+// distinct for the 2x-upsampled tap (PIX = 68 gave (px + q) mod 16, 2-way conflicts).
+constexpr int PIX = 72;
 constexpr int TILE_H = 8, TILE_W = 16;
 __constant__ const int kMaxRows[4] = {6, 4, 3, 3};
 __constant__ const int kMaxCols[4] = {10, 6, 4, 3};

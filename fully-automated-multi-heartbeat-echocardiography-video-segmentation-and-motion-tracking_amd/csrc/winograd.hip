@@ -154,10 +154,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int nt = 0; nt < NT; ++nt) acc[j][m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // ---- prologue: raw(0..2), U(0..1); transform(0)
+  // (the sched_barriers pin the issue order the counted vmcnt below relies on)
   issue_raw(0, 0);
+  __builtin_amdgcn_sched_barrier(0);
   load_u(0, u0);
+  __builtin_amdgcn_sched_barrier(0);
   issue_raw(nchunk > 1 ? 1 : -1, 1);
+  __builtin_amdgcn_sched_barrier(0);
   load_u(nchunk > 1 ? 1 : 0, u1);
+  __builtin_amdgcn_sched_barrier(0);
   issue_raw(nchunk > 2 ? 2 : -1, 2);
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_waitcnt(0x0F70 | (20 & 15) | ((20 >> 4) << 14));  // vmcnt(20): raw(0) landed

@@ -76,6 +76,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const void* src = (k < nchunk && d_off[j] >= 0) ? (const void*)(x + (size_t)d_off[j] + k * 8) : p.zero;
+      if constexpr ((KO & 32) != 0)  // timing probe: same bytes, fully coalesced (wrong data)
+        src = (const void*)(x + ((size_t)(blk & 4095) * 8 + (k & 7)) * 2048 + (size_t)((wid + 4 * j) * 64 + lane) * 4);
       dma16(src, raw + stage * Q_RAW + (wid + 4 * j) * 1024);
     }
   };
@@ -140,10 +142,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
   // prologue: raw(0), U(0), raw(1), U(1), raw(2); transform(0). Per chunk each wave issues exactly
   // 2 DMAs + 6 U loads (past-the-end fetches read the zero block / chunk 0), so the counts are exact.
+  // (the sched_barriers pin the issue order the counted vmcnt below relies on)
   issue_raw(0, 0);
+  __builtin_amdgcn_sched_barrier(0);
   load_u(0, u0);
+  __builtin_amdgcn_sched_barrier(0);
   issue_raw(1, 1);
+  __builtin_amdgcn_sched_barrier(0);
   load_u(1, u1);
+  __builtin_amdgcn_sched_barrier(0);
   issue_raw(2, 2);
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_waitcnt(0x0F70 | (16 & 15) | ((16 >> 4) << 14));  // vmcnt(16): raw(0) landed
@@ -161,15 +168,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    issue_raw(k + 3, k % 3);
-    load_u(k + 2, un);
-    __builtin_amdgcn_sched_barrier(0);
     const char* vb = vbuf + (k & 1) * Q_V + a_off;
     f32x4 a[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) a[j] = *reinterpret_cast<const f32x4*>(vb + (4 * wid + j) * (Q_BT * 32));
     float d[16];  // raw(k+1) -> V((k+1)&1); branch-free (the last chunk transforms the unused fetch)
     transform_read((k + 1) % 3, d);
+    // fetches for chunks k+3 (raw) / k+2 (U), issued after this chunk's LDS reads so that they can
+    // ride in the first MFMA gaps instead of delaying the first MFMA
+    issue_raw(k + 3, k % 3);
+    load_u(k + 2, un);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -187,6 +195,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     transform_write(d, (k + 1) & 1);
     if constexpr (KO == 0) {
 #pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (2 LDS-DMAs, 6 U loads)
+      }
+#pragma unroll
       for (int g = 0; g < 16; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
         __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
@@ -196,7 +209,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
         __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
     }
   };
   if constexpr (NCH > 0) {
@@ -335,6 +348,7 @@ hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 6: return launch_q<8, 6>(p, s);
     case 8: return launch_q<8, 8>(p, s);
     case 15: return launch_q<8, 15>(p, s);
+    case 32: return launch_q<8, 32>(p, s);
   }
   return hipErrorInvalidValue;
 }

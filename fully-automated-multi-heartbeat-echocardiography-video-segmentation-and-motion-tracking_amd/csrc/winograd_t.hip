@@ -138,10 +138,14 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) vo
 
   // Chunk k: raw(k+2) is fetched at its start, U(k+2) at its end (the U slot is read until then);
   // at the top of chunk k, raw(k+1) and U(k) must have landed: only U(k+1)'s 2 DMAs are newer.
-  issue_raw(0, 0);
+  issue_raw(0, 0);  // (the sched_barriers pin the issue order the counted vmcnt relies on)
+  __builtin_amdgcn_sched_barrier(0);
   issue_u(0, 0);
+  __builtin_amdgcn_sched_barrier(0);
   issue_raw(1, 1);
+  __builtin_amdgcn_sched_barrier(0);
   issue_u(1, 1);
+  __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_waitcnt(0x0F70 | 6);  // vmcnt(6): raw(0) landed
   __builtin_amdgcn_s_barrier();
   transform(0);
@@ -370,11 +374,16 @@ __global__ __launch_bounds__(T2_NTHR) void conv_winot2(ConvParams p, int n_co, i
     for (int n = 0; n < 2; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // prologue: raw(0), U(0), raw(1), U(1), raw(2); transform(0)
-  issue_raw(0, 0);
+  issue_raw(0, 0);  // (the sched_barriers pin the issue order the counted vmcnt relies on)
+  __builtin_amdgcn_sched_barrier(0);
   issue_u(0, 0);
+  __builtin_amdgcn_sched_barrier(0);
   issue_raw(1, 1);
+  __builtin_amdgcn_sched_barrier(0);
   issue_u(1, 1);
+  __builtin_amdgcn_sched_barrier(0);
   issue_raw(2, 2);
+  __builtin_amdgcn_sched_barrier(0);
   if (two_raw)
     __builtin_amdgcn_s_waitcnt(0x0F70 | 6);  // vmcnt(2 + 2*2): raw(0) landed
   else
@@ -396,8 +405,6 @@ __global__ __launch_bounds__(T2_NTHR) void conv_winot2(ConvParams p, int n_co, i
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    issue_raw(k + 3, k % 3);
-    __builtin_amdgcn_sched_barrier(0);
     const float* vb = reinterpret_cast<const float*>(vbuf + (k & 1) * T2_V) + e * (T2_BT * 8);
     const float* ub = reinterpret_cast<const float*>(ubuf + (k & 1) * T2_U) + e * 512;
     f32x2 a[6], b[2];
@@ -407,6 +414,7 @@ __global__ __launch_bounds__(T2_NTHR) void conv_winot2(ConvParams p, int n_co, i
     for (int n = 0; n < 2; ++n) b[n] = *reinterpret_cast<const f32x2*>(ub + swz(16 * n + b_row, 2 * q));
     float d[6];
     transform_read((k + 1) % 3, d);
+    issue_raw(k + 3, k % 3);  // after this chunk's LDS reads: rides in the first MFMA gaps
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -421,6 +429,11 @@ __global__ __launch_bounds__(T2_NTHR) void conv_winot2(ConvParams p, int n_co, i
     transform_write(d, (k + 1) & 1);
     if constexpr (KO == 0) {
 #pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (raw LDS-DMA)
+      }
+#pragma unroll
       for (int g = 0; g < 6; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
         __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
@@ -430,7 +443,7 @@ __global__ __launch_bounds__(T2_NTHR) void conv_winot2(ConvParams p, int n_co, i
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
         __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 10, 0);
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of its U(k) half are done
     __builtin_amdgcn_sched_barrier(0);
