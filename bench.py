@@ -4,8 +4,9 @@ One step = the hot path over one batch of synthetic EchoNet-shaped input, inputs
 in HBM: per GPU one 200-frame 112x112 video, 5 temporally shifted passes (30 clips of 32 frames,
 BASELINE config[1]), clips built on the device, R(2+1)D encoder-decoder forward on every clip,
 softmax -> temporal re-interpolation -> argmax per pass, SIMPLE label fusion per frame. With N GPUs
-the batch is N videos; the global clip list is sharded clip-wise across ranks, per-clip logits are
-all-gathered over RCCL and each rank fuses the videos it owns (weak scaling).
+the batch is N videos; the global clip list is sharded clip-wise across ranks, each rank fuses the
+videos it owns and per-clip logits computed away from their owner move by one RCCL all_to_all (none
+at one video per GPU: weak scaling).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 via torch.distributed.run.
 Prints one JSON line on rank 0.
@@ -189,7 +190,7 @@ def main():
                                    "(30 x 32-frame clips) + per-frame SIMPLE label fusion",
                        "videos_per_gpu": args.videos_per_gpu, "frames": args.frames, "fuse": args.fuse,
                        "step": args.step, "clips_per_step": clips_per_step, "batch_size": args.batch_size,
-                       "parallelism": f"clip-shard x{world}, all-gather of per-clip logits"},
+                       "parallelism": f"clip-shard x{world}, owner all_to_all of per-clip logits (skipped when every video is rank-local)"},
             "roofline": kernel_roofline(ktimes, FP32_PEAK_TFLOPS, "fp32"),
             "forward": {"achieved_tflops": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS,
                         "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "gflop_per_clip": GFLOP_PER_CLIP,

@@ -2,10 +2,15 @@
 
 Every 32-frame clip of every temporally shifted pass of every video is independent
 (src/fuse_utils.py:45-61), so the global clip list is partitioned into contiguous blocks, one per
-rank; each rank runs the encoder-decoder on its block only, and one all-gather of the per-clip
-segmentation logits (2 x 32 x H x W fp32 per clip) over RCCL/xGMI gives every rank every clip
-before fusion. Fusion is then split by video (video v is fused by rank v % world). The result is
-bit-identical to the 1-GPU run because the per-clip computation is identical; only placement moves.
+rank; each rank runs the encoder-decoder on its block only. Fusion is split by video (video v is
+fused by its owner, rank v % world), so a clip's segmentation logits (2 x 32 x H x W fp32) only have
+to reach that one rank: one all_to_all over RCCL/xGMI moves exactly the clips computed away from
+their owner ("owner-gather"). When every video's clips are computed by its
+owner -- the weak-scaling case of one video per GPU -- nothing crosses xGMI and the collective is
+skipped on every rank (the decision is a pure function of the global plan, so all ranks agree).
+The result is bit-identical to the 1-GPU run: the per-clip computation is placement independent.
+``all_gather_clips`` / ``run_clip_shard`` (every rank gets every clip) remain for callers that need
+all logits everywhere.
 """
 import torch
 import torch.distributed as dist
@@ -62,6 +67,42 @@ def run_clip_shard(n_total, rank, world, compute, empty):
     return all_gather_clips(local.contiguous(), n_total, rank, world)
 
 
+def owner_of_clips(plans, world):
+    """Owner rank of every global clip (the owner of its video: video v -> v % world)."""
+    own = []
+    for vi, p in enumerate(plans):
+        own.extend([vi % world] * p["n"])
+    return own
+
+
+def exchange_to_owners(local, owners, rank, world, group=None):
+    """Route per-clip rows to their owners. ``local`` holds rows [lo, hi) of the global clip list
+    (this rank's shard_bounds block); ``owners[g]`` is the owner rank of global clip g. Returns the
+    rows of every clip this rank owns, in global clip order. One all_to_all_single; skipped when no
+    clip is computed away from its owner (all ranks derive that from the same plan)."""
+    n_total = len(owners)
+    blocks = [shard_bounds(n_total, r, world) for r in range(world)]
+    # counts[s][o] = clips computed by rank s for owner o
+    counts = [[0] * world for _ in range(world)]
+    for s_, (lo, hi) in enumerate(blocks):
+        for g in range(lo, hi):
+            counts[s_][owners[g]] += 1
+    lo, hi = blocks[rank]
+    if world == 1 or all(counts[s_][o] == 0 for s_ in range(world) for o in range(world) if s_ != o):
+        keep = [g - lo for g in range(lo, hi) if owners[g] == rank]
+        if len(keep) == hi - lo:
+            return local
+        return local[torch.tensor(keep, dtype=torch.long, device=local.device)]
+    order = sorted(range(lo, hi), key=lambda g: (owners[g], g))  # by destination, then global order
+    send = local[torch.tensor([g - lo for g in order], dtype=torch.long, device=local.device)] if order else local
+    send_sizes = counts[rank]
+    recv_sizes = [counts[s_][rank] for s_ in range(world)]
+    out = torch.empty((sum(recv_sizes),) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    dist.all_to_all_single(out, send.contiguous(), output_split_sizes=recv_sizes, input_split_sizes=send_sizes,
+                           group=group)
+    return out  # source blocks are in rank order and each is in global order: global order overall
+
+
 def segment_videos_sharded(videos_dev, model, num_clips=5, step=1, fuse_method="simple", interpolate_last=True,
                            rank=0, world=1, batch_size=None, clip_fn=None):
     """Fuse a batch of device videos (each (3,T,H,W)) with clips sharded over ranks.
@@ -83,12 +124,15 @@ def segment_videos_sharded(videos_dev, model, num_clips=5, step=1, fuse_method="
         return clip_fn(clips) if clip_fn else FU.run_model(model, clips, batch_size)
 
     empty = torch.empty((0, 2, FU.CLIP, h, w), device=dev, dtype=torch.float32)
-    logits = run_clip_shard(n_total, rank, world, compute, empty)
-    out = {}
+    lo, hi = shard_bounds(n_total, rank, world)
+    local = compute(lo, hi) if hi > lo else empty
+    mine = exchange_to_owners(local.contiguous(), owner_of_clips(plans, world), rank, world)
+    out, at = {}, 0
     for vi, p in enumerate(plans):
         if vi % world != rank:
             continue
-        lg = logits[p["offset"]: p["offset"] + p["n"]]
+        lg = mine[at: at + p["n"]]
+        at += p["n"]
         labels = FU.pass_labels(lg, p["clip0"], p["T"], step, interpolate_last)
         out[vi] = FU.fuse_votes(labels, step, fuse_method)
     return out

@@ -176,3 +176,39 @@ def test_clip_shard_all_gather_gloo(world, n_total):
     ref = np.arange(n_total, dtype=np.float32)[:, None, None] * 10 + np.arange(6, dtype=np.float32).reshape(1, 2, 3)
     for r in range(world):
         np.testing.assert_array_equal(res[r], ref)
+
+
+def _owner_worker(rank, world, port, sizes, q):
+    import torch.distributed as dist
+    from clasfv_amd.dist import exchange_to_owners, shard_bounds
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        owners = [vi % world for vi, n in enumerate(sizes) for _ in range(n)]
+        lo, hi = shard_bounds(len(owners), rank, world)
+        local = torch.arange(lo, hi, dtype=torch.float32)[:, None] * torch.ones(1, 3)  # row g = g
+        q.put((rank, exchange_to_owners(local, owners, rank, world).numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sizes", [(2, [6, 5, 7]), (3, [1, 1, 1, 1, 1]), (2, [30, 30]), (3, [4, 0, 9, 2])])
+def test_owner_exchange_gloo(world, sizes):
+    """Owner exchange (all_to_all of per-clip rows to the rank fusing their video): every rank gets
+    exactly the rows of the videos it owns, in global order; the one-video-per-rank case moves nothing."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_owner_worker, args=(r, world, port, sizes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    offs = np.cumsum([0] + sizes)
+    for r in range(world):
+        want = np.concatenate([np.arange(offs[v], offs[v + 1]) for v in range(len(sizes)) if v % world == r] or
+                              [np.zeros(0)]).astype(np.float32)
+        np.testing.assert_array_equal(res[r][:, 0], want)
