@@ -67,13 +67,29 @@ def to_device_video(video, device):
     return v.to(device, torch.float32).contiguous()
 
 
+_TABLES = {}
+
+
+def _device_table(table, device):
+    """Device int32 copy of a clip table, cached: a fresh pageable host->device copy per call would
+    make every video wait for the copy engine (and the host for the stream) before its clips build."""
+    key = (str(device), tuple(table))
+    t = _TABLES.get(key)
+    if t is None:
+        if len(_TABLES) > 256:
+            _TABLES.clear()
+        t = torch.tensor(np.asarray(table, np.int32).reshape(-1), device=device)
+        _TABLES[key] = t
+    return t
+
+
 def build_clips(video_dev, table, interpolate_last=True):
     """(n,3,32,H,W) clips on the device for a [(shift, first_frame)] table."""
     if video_dev.dim() != 4 or video_dev.shape[0] != 3:
         raise ValueError(f"expected a (3,T,H,W) video, got {tuple(video_dev.shape)}")
     video_dev = video_dev.to(torch.float32).contiguous()  # the ABI takes dense row-major buffers
     _, t, h, w = video_dev.shape
-    tab = torch.tensor(np.asarray(table, np.int32).reshape(-1), device=video_dev.device)
+    tab = _device_table(table, video_dev.device)
     clips = torch.empty((len(table), 3, CLIP, h, w), device=video_dev.device, dtype=torch.float32)
     lib = _lib.load()
     _lib.check(lib.clasfv_build_clips(_lib.ptr(video_dev), t, h, w, _lib.ptr(tab), len(table), int(bool(interpolate_last)),
