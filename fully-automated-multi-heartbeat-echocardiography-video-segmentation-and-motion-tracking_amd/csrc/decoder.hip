@@ -24,16 +24,19 @@ namespace {
 // distinct for the 2x-upsampled tap (PIX = 68 gave (px + q) mod 16, 2-way conflicts).
 constexpr int PIX = 72;
 constexpr int TILE_H = 8, TILE_W = 16;
+// Source window bounds of one 8x16-voxel tile per tap (tap i: scale (in-1)/(out-1) < 2^-(i+1), so
+// 8 rows touch at most floor(7 s) + 3 source rows, 16 columns floor(15 s) + 3).
 __constant__ const int kMaxRows[4] = {6, 4, 3, 3};
 __constant__ const int kMaxCols[4] = {10, 6, 4, 3};
 // tap 0 (stem + layer1) keeps the clip's frame rate: its temporal scale is exactly 1, one frame.
 constexpr int kFrames[4] = {1, 2, 2, 2};
-constexpr int kPixOff[5] = {0, 1 * 6 * 10, 1 * 6 * 10 + 2 * 4 * 6, 1 * 6 * 10 + 2 * 4 * 6 + 2 * 3 * 4,
-                            1 * 6 * 10 + 2 * 4 * 6 + 2 * 3 * 4 + 2 * 3 * 3};
+constexpr int kTapPix[4] = {1 * 6 * 10, 2 * 4 * 6, 2 * 3 * 4, 2 * 3 * 3};
+constexpr int kPixOff[5] = {0, kTapPix[0], kTapPix[0] + kTapPix[1], kTapPix[0] + kTapPix[1] + kTapPix[2],
+                            kTapPix[0] + kTapPix[1] + kTapPix[2] + kTapPix[3]};
 constexpr int STAGE_FLOATS = kPixOff[4] * PIX;
 // per-thread 16-byte staging loads per tap: ceil(frames * rows * cols * 16 / 256)
-constexpr int kLoads[4] = {(1 * 6 * 10 * 16 + 255) / 256, (2 * 4 * 6 * 16 + 255) / 256, (2 * 3 * 4 * 16 + 255) / 256,
-                           (2 * 3 * 3 * 16 + 255) / 256};
+constexpr int kLoads[4] = {(kTapPix[0] * 16 + 255) / 256, (kTapPix[1] * 16 + 255) / 256, (kTapPix[2] * 16 + 255) / 256,
+                           (kTapPix[3] * 16 + 255) / 256};
 constexpr int kLoadOff[4] = {0, kLoads[0], kLoads[0] + kLoads[1], kLoads[0] + kLoads[1] + kLoads[2]};
 constexpr int kLoadsTotal = kLoads[0] + kLoads[1] + kLoads[2] + kLoads[3];
 
@@ -50,6 +53,9 @@ __device__ inline void src_index(float s, int dst, int in, int& i0, int& i1, flo
   l0 = 1.f - l1;
 }
 
+// KO != 0 only in tools/convbench.hip (knock-out timing builds): bit 1 no interpolation, 2 no staging
+// loads, 4 no comb_2/head MFMAs, 8 no output stores.
+template <int KO = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void decoder_kernel(DecParams p) {
   extern __shared__ __align__(16) float smem[];
   float* stage = smem;  // STAGE_FLOATS
@@ -96,7 +102,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
     for (int k = 0; k < kLoads[i]; ++k) {
       const int e = tid + 256 * k;
-      if (e < total) {
+      if constexpr ((KO & 2) != 0) {
+        buf[kLoadOff[i] + k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      } else if (e < total) {
         const int c4 = e & 15, px = e >> 4;
         const int cc = px % w.nc, tmp = px / w.nc;
         const int rr = tmp % w.nr, ff = tmp / w.nr;
@@ -137,6 +145,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     for (int c = 0; c < 4; ++c) h1[c] = *reinterpret_cast<const f32x4*>(p.b1 + 16 * c + 4 * q);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      if constexpr ((KO & 1) != 0) break;
       const DecTap& tp = p.tap[i];
       const Win& w = win[i];
       int x0, x1, y0, y1;
@@ -187,8 +196,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[c][j], h1[c][j], acc[nt], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+          if constexpr ((KO & 4) != 0)
+            acc[nt][j] += wa[c][j] * h1[c][j];
+          else
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[c][j], h1[c][j], acc[nt], 0, 0, 0);
+        }
       // acc[nt][r] = h2^T[ch = 16nt + 4q + r][voxel l16]
       const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
 #pragma unroll
@@ -201,9 +214,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[nt][r], out, 0, 0, 0);
+      for (int r = 0; r < 4; ++r) {
+        if constexpr ((KO & 4) != 0)
+          out[r] += wh[nt][r] * acc[nt][r];
+        else
+          out = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[nt][r], out, 0, 0, 0);
+      }
     // 5. out[r] = head (4q + r) at voxel (hr, w0 + l16)
-    if (q < 2) {
+    if constexpr ((KO & 8) != 0) {
+      if (out[0] + out[1] + out[2] + out[3] == 1.2345f) p.seg[tid] = out[0];
+    } else if (q < 2) {
       const size_t pix = (size_t)t * HW + (size_t)hr * p.W + (w0 + l16);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -221,16 +241,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 
 }  // namespace
 
-hipError_t launch_decoder(const DecParams& p, hipStream_t s) {
+template <int KO>
+static hipError_t launch_dec(const DecParams& p, hipStream_t s) {
   if (p.tap[0].T != p.T) return hipErrorInvalidValue;  // tap 0 is staged as a single frame
   dim3 grid((p.H / TILE_H) * (p.W / TILE_W), p.T, p.N);
   const size_t lds = (size_t)STAGE_FLOATS * 4;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)decoder_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void*)decoder_kernel<KO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(decoder_kernel, grid, dim3(256), lds, s, p);
+  hipLaunchKernelGGL(decoder_kernel<KO>, grid, dim3(256), lds, s, p);
   return hipGetLastError();
 }
+
+hipError_t launch_decoder(const DecParams& p, hipStream_t s) { return launch_dec<0>(p, s); }
+
+#ifdef CLASFV_KNOCKOUTS
+hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko) {
+  switch (ko) {
+    case 0: return launch_dec<0>(p, s);
+    case 1: return launch_dec<1>(p, s);
+    case 2: return launch_dec<2>(p, s);
+    case 3: return launch_dec<3>(p, s);
+    case 4: return launch_dec<4>(p, s);
+    case 8: return launch_dec<8>(p, s);
+    case 12: return launch_dec<12>(p, s);
+    case 15: return launch_dec<15>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+#endif

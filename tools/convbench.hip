@@ -15,6 +15,10 @@
 hipError_t launch_wino_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko);
+hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
+
+// decoder: N clips of T x H x W, taps at (T, H/2, W/2), (T/2, H/4, W/4), (T/4, H/8), (T/8, H/16)
+static int run_decoder(int N, int T, int H, int W, int iters, const std::vector<int>& kos);
 
 #define CK(x)                                                                  \
   do {                                                                         \
@@ -44,6 +48,12 @@ int main(int argc, char** argv) {
     return 2;
   }
   const char* kind = argv[1];
+  if (!strcmp(kind, "dec")) {
+    std::vector<int> k2;
+    for (int i = 7; i < argc; ++i) k2.push_back(atoi(argv[i]));
+    if (k2.empty()) k2.push_back(0);
+    return run_decoder(atoi(argv[2]), atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), argc > 6 ? atoi(argv[6]) : 20, k2);
+  }
   const int N = atoi(argv[2]), T = atoi(argv[3]), H = atoi(argv[4]), W = atoi(argv[5]);
   const int Cin = atoi(argv[6]), Cout = atoi(argv[7]);
   const int iters = argc > 8 ? atoi(argv[8]) : 20;
@@ -109,5 +119,52 @@ int main(int argc, char** argv) {
   for (size_t v = 0; v < kos.size(); ++v)
     printf("%s%-6s N=%d T=%d H=%d W=%d Cin=%d Cout=%d ko=%-3d  %8.3f ms  %7.1f TF(alg)\n", p.res ? "res   " : "nores ",
            kind, N, T, H, W, Cin, Cout, kos[v], best[v], gflop / best[v]);
+  return 0;
+}
+
+static float scale_ac(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
+
+static int run_decoder(int N, int T, int H, int W, int iters, const std::vector<int>& kos) {
+  DecParams d;
+  memset(&d, 0, sizeof(d));
+  const int div[4][2] = {{1, 2}, {2, 4}, {4, 8}, {8, 16}};
+  for (int i = 0; i < 4; ++i) {
+    DecTap& t = d.tap[i];
+    t.T = T / div[i][0];
+    t.H = H / div[i][1];
+    t.W = W / div[i][1];
+    t.st = scale_ac(t.T, T);
+    t.sh = scale_ac(t.H, H);
+    t.sw = scale_ac(t.W, W);
+    t.p = (const float*)dev_random((size_t)N * t.T * t.H * t.W * 64, -1.f, 1.f, 10 + i);
+  }
+  d.b1 = (const float*)dev_random(64, -0.1f, 0.1f, 20);
+  d.w2 = (const float*)dev_random(64 * 64, -0.1f, 0.1f, 21);
+  d.b2 = (const float*)dev_random(64, -0.1f, 0.1f, 22);
+  d.wh = (const float*)dev_random(8 * 64, -0.1f, 0.1f, 23);
+  d.bh = (const float*)dev_random(8, -0.1f, 0.1f, 24);
+  CK(hipMalloc((void**)&d.seg, (size_t)N * 2 * T * H * W * 4));
+  CK(hipMalloc((void**)&d.mot, (size_t)N * 4 * T * H * W * 4));
+  d.N = N, d.T = T, d.H = H, d.W = W;
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int ko : kos)
+    for (int i = 0; i < 5; ++i) CK(launch_decoder_ko(d, s, ko));
+  std::vector<float> best(kos.size(), 1e30f);
+  for (int rep = 0; rep < 3; ++rep)
+    for (size_t v = 0; v < kos.size(); ++v) {
+      CK(hipEventRecord(a, s));
+      for (int i = 0; i < iters; ++i) CK(launch_decoder_ko(d, s, kos[v]));
+      CK(hipEventRecord(b, s));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      if (ms / iters < best[v]) best[v] = ms / iters;
+    }
+  for (size_t v = 0; v < kos.size(); ++v)
+    printf("dec    N=%d T=%d H=%d W=%d ko=%-3d  %8.3f ms\n", N, T, H, W, kos[v], best[v]);
   return 0;
 }
