@@ -137,12 +137,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     wh[nt] = *reinterpret_cast<const f32x4*>(p.wh + (l16 & 7) * 64 + 16 * nt + 4 * q);
     if (l16 >= 8) wh[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-#pragma unroll 1
+  // Both voxel rows of the wave are interpolated first, then share every W2 fragment load (W2 is
+  // re-read from L1/L2 once per wave rather than once per row: the loads were the kernel's fixed cost).
+  f32x4 h1[2][4];
+#pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     const int hr = h0 + 2 * wid + mt;
-    f32x4 h1[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) h1[c] = *reinterpret_cast<const f32x4*>(p.b1 + 16 * c + 4 * q);
+    for (int c = 0; c < 4; ++c) h1[mt][c] = *reinterpret_cast<const f32x4*>(p.b1 + 16 * c + 4 * q);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if constexpr ((KO & 1) != 0) break;
@@ -168,57 +170,64 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         const float w00 = a0 * lx0, w01 = a0 * lx1, w10 = a1 * lx0, w11 = a1 * lx1;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          h1[c] += *reinterpret_cast<const f32x4*>(p00 + 16 * c) * w00;
-          h1[c] += *reinterpret_cast<const f32x4*>(p01 + 16 * c) * w01;
-          h1[c] += *reinterpret_cast<const f32x4*>(p10 + 16 * c) * w10;
-          h1[c] += *reinterpret_cast<const f32x4*>(p11 + 16 * c) * w11;
+          h1[mt][c] += *reinterpret_cast<const f32x4*>(p00 + 16 * c) * w00;
+          h1[mt][c] += *reinterpret_cast<const f32x4*>(p01 + 16 * c) * w01;
+          h1[mt][c] += *reinterpret_cast<const f32x4*>(p10 + 16 * c) * w10;
+          h1[mt][c] += *reinterpret_cast<const f32x4*>(p11 + 16 * c) * w11;
         }
       }
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) h1[c][j] = fmaxf(h1[c][j], 0.f);
+      for (int j = 0; j < 4; ++j) h1[mt][c][j] = fmaxf(h1[mt][c][j], 0.f);
+  }
 
-    // 3. h2^T[n][v] = sum_k W2[n][k] h1[v][k]; MFMA j of lane group q covers k = 16c + 4q + j
-    // (W2 rows of the next 16-channel tile are prefetched while the current one runs on MFMA)
-    f32x4 acc[4], wa[4], wn[4];
+  // 3. h2^T[n][v] = sum_k W2[n][k] h1[v][k]; MFMA j of lane group q covers k = 16c + 4q + j
+  // (W2 rows of the next 16-channel tile are prefetched while the current one runs on MFMA)
+  f32x4 acc[2][4], wa[4], wn[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) wa[c] = *reinterpret_cast<const f32x4*>(p.w2 + l16 * 64 + 16 * c + 4 * q);
+  for (int c = 0; c < 4; ++c) wa[c] = *reinterpret_cast<const f32x4*>(p.w2 + l16 * 64 + 16 * c + 4 * q);
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (nt < 3) {
+  for (int nt = 0; nt < 4; ++nt) {
+    if (nt < 3) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-          wn[c] = *reinterpret_cast<const f32x4*>(p.w2 + ((nt + 1) * 16 + l16) * 64 + 16 * c + 4 * q);
-      }
+      for (int c = 0; c < 4; ++c)
+        wn[c] = *reinterpret_cast<const f32x4*>(p.w2 + ((nt + 1) * 16 + l16) * 64 + 16 * c + 4 * q);
+    }
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if constexpr ((KO & 4) != 0)
-            acc[nt][j] += wa[c][j] * h1[c][j];
+            acc[mt][nt][j] += wa[c][j] * h1[mt][c][j];
           else
-            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[c][j], h1[c][j], acc[nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[c][j], h1[mt][c][j], acc[mt][nt], 0, 0, 0);
         }
-      // acc[nt][r] = h2^T[ch = 16nt + 4q + r][voxel l16]
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
+      // acc[mt][nt][r] = h2^T[ch = 16nt + 4q + r][voxel l16]
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[nt][r] = fmaxf(acc[nt][r] + bb[r], 0.f);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) wa[c] = wn[c];
+      for (int r = 0; r < 4; ++r) acc[mt][nt][r] = fmaxf(acc[mt][nt][r] + bb[r], 0.f);
     }
-    // 4. heads^T[co][v] = sum_k Wh[co][k] h2^T[k][v]; the accumulator layout is the B operand
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wa[c] = wn[c];
+  }
+  // 4. heads^T[co][v] = sum_k Wh[co][k] h2^T[k][v]; the accumulator layout is the B operand
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int hr = h0 + 2 * wid + mt;
     f32x4 out = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         if constexpr ((KO & 4) != 0)
-          out[r] += wh[nt][r] * acc[nt][r];
+          out[r] += wh[nt][r] * acc[mt][nt][r];
         else
-          out = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[nt][r], out, 0, 0, 0);
+          out = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[mt][nt][r], out, 0, 0, 0);
       }
     // 5. out[r] = head (4q + r) at voxel (hr, w0 + l16)
     if constexpr ((KO & 8) != 0) {
