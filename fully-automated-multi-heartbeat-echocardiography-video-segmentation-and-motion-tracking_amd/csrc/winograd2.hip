@@ -27,12 +27,17 @@ __device__ inline void dma16(const void* src, void* lds_dst) {
 }
 
 // conv_wino_q: block = 4 waves (wave = transform row i) x 2 patches (32 tiles) x 48 output channels,
-// 2 blocks per CU (56 KB LDS); U operands in registers, fetched two chunks ahead (3-way rotation);
-// raw ring 3 x 8 KB, V double-buffered; one barrier per chunk.
+// 2 blocks per CU (72 KB LDS); U operands in registers, fetched two chunks ahead (3-way rotation);
+// raw ring 3 x 8 KB, V ring 3 x 16 KB so that each chunk's V operands are read into registers one
+// chunk ahead (2-way rotation) and the MFMAs start right after the chunk barrier (2.51 -> 2.43 ms on
+// layer1). One barrier per chunk.
+// Knock-out probes (tools/convbench.sh): U operands replaced by lane-varying register values cost
+// the same as the loads (KO 128), and loading chunk 0's U every chunk (L1-resident, KO 64) is no
+// faster: the U fetch is not a bottleneck; the MFMA issue stream itself is (SQ_VALU_MFMA_BUSY 57 %).
 constexpr int Q_BT = 32;
 constexpr int Q_RAW = 8 * 1024;       // 8 DMA wave-instructions (400 slots used)
 constexpr int Q_V = 16 * Q_BT * 32;   // 16 KB
-constexpr int Q_LDS = 3 * Q_RAW + 2 * Q_V;
+constexpr int Q_LDS = 3 * Q_RAW + 3 * Q_V;  // 72 KB: 2 blocks per CU
 
 template <int NCH, int KO = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino_q(ConvParams p, int n_co,
@@ -89,7 +94,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int nt = 0; nt < 3; ++nt) u[nt][0] = u[nt][1] = f32x4{1.f, 1.f, 1.f, 1.f} * (float)k;
       return;
     }
-    const float* b = ub + (size_t)(k < nchunk ? k : 0) * 4 * CO * 32;
+    if constexpr (KO & 128) {  // timing probe: lane-varying operands without loads
+#pragma unroll
+      for (int nt = 0; nt < 3; ++nt)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            u[nt][h][c] = (float)(((unsigned)lane * 2654435761u + (unsigned)k * 40503u + nt * 97 + h * 13 + c) & 0xffffu) * 1e-4f;
+      return;
+    }
+    // KO & 64: every chunk re-reads chunk 0's operands (L1-resident, same values) -- timing probe
+    const float* b = (KO & 64) ? ub : ub + (size_t)(k < nchunk ? k : 0) * 4 * CO * 32;
 #pragma unroll
     for (int nt = 0; nt < 3; ++nt)
 #pragma unroll
@@ -131,7 +147,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
   };
 
-  f32x4 u0[3][2], u1[3][2], u2[3][2];
+  f32x4 uu[3][3][2];  // U operands, 3-way rotation (chunk k uses uu[k % 3])
+  f32x4 aa[2][4];     // V (A) operands, 2-way rotation (chunk k uses aa[k & 1])
   f32x4 acc[4][2][3];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -140,20 +157,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int nt = 0; nt < 3; ++nt) acc[j][m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: raw(0), U(0), raw(1), U(1), raw(2); transform(0). Per chunk each wave issues exactly
-  // 2 DMAs + 6 U loads (past-the-end fetches read the zero block / chunk 0), so the counts are exact.
-  // (the sched_barriers pin the issue order the counted vmcnt below relies on)
+  const int a_off = (l16 * 4 + q) * 16;
+  auto read_a = [&](int vstage, f32x4 (&a)[4]) __attribute__((always_inline)) {
+    const char* vb = vbuf + vstage * Q_V + a_off;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = *reinterpret_cast<const f32x4*>(vb + (4 * wid + j) * (Q_BT * 32));
+  };
+  // Pipeline: chunk k multiplies V(k) (operands read into registers during chunk k-1), reads V(k+1),
+  // transforms raw(k+2) into V stage (k+2) % 3 and fetches raw(k+4) / U(k+2). The first MFMA after
+  // the chunk barrier therefore never waits for LDS.
+  // prologue: raw(0..2), U(0); transform raw(0); raw(3) (into raw(0)'s stage, after a barrier), U(1);
+  // transform raw(1). Per chunk each wave then issues exactly 2 DMAs + 6 U loads (past-the-end
+  // fetches read the zero block / chunk 0), so the counted vmcnt values are exact.
+  // (the sched_barriers pin the issue order the counted vmcnt relies on)
   issue_raw(0, 0);
-  __builtin_amdgcn_sched_barrier(0);
-  load_u(0, u0);
   __builtin_amdgcn_sched_barrier(0);
   issue_raw(1, 1);
   __builtin_amdgcn_sched_barrier(0);
-  load_u(1, u1);
-  __builtin_amdgcn_sched_barrier(0);
   issue_raw(2, 2);
   __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_waitcnt(0x0F70 | (16 & 15) | ((16 >> 4) << 14));  // vmcnt(16): raw(0) landed
+  load_u(0, uu[0]);
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0x0F70 | 10);  // vmcnt(10): raw(0) landed
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   {
@@ -161,22 +186,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     transform_read(0, d);
     transform_write(d, 0);
   }
+  __builtin_amdgcn_s_waitcnt(0x0F70 | 8);  // vmcnt(8): raw(1) landed
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();  // every wave has read raw stage 0
+  __builtin_amdgcn_sched_barrier(0);
+  issue_raw(3, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  load_u(1, uu[1]);
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    float d[16];
+    transform_read(1, d);
+    transform_write(d, 1);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own V stores done
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  read_a(0, aa[0]);
 
-  const int a_off = (l16 * 4 + q) * 16;
-  auto step = [&](int k, f32x4 (&uc)[3][2], f32x4 (&un)[3][2]) __attribute__((always_inline)) {
-    __builtin_amdgcn_s_waitcnt(0x0070 | 8);  // vmcnt(8): raw(k+1), U(k) landed; lgkmcnt(0): own V stores done
+  auto step = [&](int k, f32x4 (&uc)[3][2], f32x4 (&un)[3][2], f32x4 (&ac)[4], f32x4 (&an)[4])
+                  __attribute__((always_inline)) {
+    // vmcnt(8): raw(k+2), U(k) landed; lgkmcnt(0): own V stores and operand reads done
+    __builtin_amdgcn_s_waitcnt(0x0070 | 8);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    const char* vb = vbuf + (k & 1) * Q_V + a_off;
-    f32x4 a[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = *reinterpret_cast<const f32x4*>(vb + (4 * wid + j) * (Q_BT * 32));
-    float d[16];  // raw(k+1) -> V((k+1)&1); branch-free (the last chunk transforms the unused fetch)
-    transform_read((k + 1) % 3, d);
-    // fetches for chunks k+3 (raw) / k+2 (U), issued after this chunk's LDS reads so that they can
-    // ride in the first MFMA gaps instead of delaying the first MFMA
-    issue_raw(k + 3, k % 3);
+    read_a((k + 1) % 3, an);
+    float d[16];  // raw(k+2) -> V((k+2)%3); branch-free (the last chunks transform unused fetches)
+    transform_read((k + 2) % 3, d);
+    issue_raw(k + 4, (k + 1) % 3);
     load_u(k + 2, un);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -187,13 +226,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
           for (int nt = 0; nt < 3; ++nt) {
             if constexpr (KO & 16)
-              acc[j][m][nt][0] += a[j][2 * m + s2] * uc[nt][j >> 1][(j & 1) * 2 + s2];
+              acc[j][m][nt][0] += ac[j][2 * m + s2] * uc[nt][j >> 1][(j & 1) * 2 + s2];
             else
-              acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][2 * m + s2], uc[nt][j >> 1][(j & 1) * 2 + s2],
+              acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[j][2 * m + s2], uc[nt][j >> 1][(j & 1) * 2 + s2],
                                                                    acc[j][m][nt], 0, 0, 0);
           }
-    transform_write(d, (k + 1) & 1);
+    transform_write(d, (k + 2) % 3);
     if constexpr (KO == 0) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // DS read (8 transform, 4 operand)
+      }
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -209,25 +253,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
         __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
   };
   if constexpr (NCH > 0) {
 #pragma unroll
-    for (int kk = 0; kk < NCH; kk += 3) {
-      step(kk, u0, u2);
-      if (kk + 1 < NCH) step(kk + 1, u1, u0);
-      if (kk + 2 < NCH) step(kk + 2, u2, u1);
-    }
+    for (int kk = 0; kk < NCH; ++kk) step(kk, uu[kk % 3], uu[(kk + 2) % 3], aa[kk & 1], aa[(kk + 1) & 1]);
   } else {
     int k = 0;
-    for (; k + 3 <= nchunk; k += 3) {
-      step(k, u0, u2);
-      step(k + 1, u1, u0);
-      step(k + 2, u2, u1);
+    for (; k + 6 <= nchunk; k += 6) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) step(k + i, uu[i % 3], uu[(i + 2) % 3], aa[i & 1], aa[(i + 1) & 1]);
     }
-    if (k < nchunk) step(k, u0, u2);
-    if (k + 1 < nchunk) step(k + 1, u1, u0);
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      if (k + i < nchunk) step(k + i, uu[i % 3], uu[(i + 2) % 3], aa[i & 1], aa[(i + 1) & 1]);
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // drain past-the-end fetches before LDS is reused
 
@@ -348,7 +388,11 @@ hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 6: return launch_q<8, 6>(p, s);
     case 8: return launch_q<8, 8>(p, s);
     case 15: return launch_q<8, 15>(p, s);
+    case 16: return launch_q<8, 16>(p, s);
+    case 24: return launch_q<8, 24>(p, s);
     case 32: return launch_q<8, 32>(p, s);
+    case 64: return launch_q<8, 64>(p, s);
+    case 128: return launch_q<8, 128>(p, s);
   }
   return hipErrorInvalidValue;
 }
