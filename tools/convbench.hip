@@ -70,11 +70,16 @@ int main(int argc, char** argv) {
   p.KT = tp ? 3 : 1, p.KH = sp ? 3 : 1, p.KW = sp ? 3 : 1;
   p.st = p.sh = p.sw = 1;
   p.pt = tp ? 1 : 0, p.ph = sp ? 1 : 0, p.pw = sp ? 1 : 0;
+  // CB_STRIDE=2: the strided first conv of a block (spatial for sp, temporal for tp; direct only)
+  if (getenv("CB_STRIDE") && !wino && !winot) {
+    if (sp) p.sh = p.sw = 2, p.Ho = (H - 1) / 2 + 1, p.Wo = (W - 1) / 2 + 1;
+    if (tp) p.st = 2, p.To = (T - 1) / 2 + 1;
+  }
   p.K = p.KT * p.KH * p.KW * Cin;
   p.Kp = (p.K + 15) / 16 * 16;
-  p.M = N * T * H * W;
+  p.M = N * p.To * p.Ho * p.Wo;
   p.relu = 1;
-  const size_t nx = (size_t)p.M * Cin, ny = (size_t)p.M * Cout;
+  const size_t nx = (size_t)N * T * H * W * Cin, ny = (size_t)p.M * Cout;
   p.x = dev_random(nx, 0.f, 1.f, 1);
   const size_t nw = wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
   p.w = dev_random(nw, -0.05f, 0.05f, 2);
@@ -85,7 +90,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&z, 256));
   CK(hipMemset(z, 0, 256));
   p.zero = z;
-  const double gflop = 2.0 * p.M * (double)Cout * Cin * p.KT * p.KH * p.KW * 1e-9;
+  const double gflop = 2.0 * p.M * (double)Cout * Cin * p.KT * p.KH * p.KW * 1e-9;  // padded Cout
   hipStream_t s;
   CK(hipStreamCreate(&s));
   hipEvent_t a, b;
