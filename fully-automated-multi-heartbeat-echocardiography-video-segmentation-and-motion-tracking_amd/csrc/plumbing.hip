@@ -12,8 +12,10 @@
 // F.interpolate in tests): scale = (float)in/out, src = fma(scale, dst + 0.5, -0.5) clamped at 0,
 // value = fma(x[i0], l0, x[i1] * l1).
 #include <float.h>
+#include <stdlib.h>
 
 #include "common.h"
+
 #include "plumbing.h"
 
 // Every fused multiply-add below is written out (fmaf) where PyTorch's CPU kernels contract one;
@@ -236,6 +238,145 @@ __global__ __launch_bounds__(SIMPLE_THREADS) void fuse_simple_kernel(const uint8
   }
 }
 
+// Fast SIMPLE for <= 16 votes: the same iteration, with each pixel's votes packed once into a 16-bit
+// mask in LDS, integer counts (exact: the Dice values and weights are those of the kernel above) and
+// one block reduction per iteration (the candidate sizes are fixed per label; the overlaps with the
+// new estimate are accumulated in the pass that computes it). 1024 threads per output frame. All
+// per-candidate loops run to the compile-time bound (guarded by nv) so the arrays stay in registers.
+constexpr int SIMPLE_FAST_THREADS = 1024;
+constexpr int SIMPLE_FAST_MAXV = 16;
+
+// Block sum of N ints per thread; every thread gets the totals in tot[].
+template <int N>
+__device__ inline void block_sum_vec(const int (&v)[N], int (*red)[2 * SIMPLE_FAST_MAXV + 1], int* tot) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    int x = v[j];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    if (lane == 0) red[wid][j] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < N) {
+    int t = 0;
+#pragma unroll
+    for (int w = 0; w < SIMPLE_FAST_THREADS / 64; ++w) t += red[w][threadIdx.x];
+    tot[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(SIMPLE_FAST_THREADS) void fuse_simple_fast_kernel(const uint8_t* __restrict__ labels, int K,
+                                                                               int T, int step, int HW,
+                                                                               uint8_t* __restrict__ fused) {
+  constexpr int MV = SIMPLE_FAST_MAXV;
+  extern __shared__ uint8_t smem_simple[];
+  uint16_t* msk = reinterpret_cast<uint16_t*>(smem_simple);  // bit idx: vote idx == 1
+  uint8_t* est = smem_simple + 2 * (size_t)HW;                // bit 0: current estimate, bit 1: label-1 result
+  __shared__ int red[SIMPLE_FAST_THREADS / 64][2 * MV + 1];
+  __shared__ int tot[2 * MV + 1];
+  const int o = blockIdx.x;
+  const int i = o == 0 ? 0 : o + step - 1;
+  const int nv = o == 0 ? 1 : n_votes(i, K, step);
+  uint8_t* out = fused + (size_t)o * HW;
+  if (nv == 1) {
+    for (int p = threadIdx.x; p < HW; p += SIMPLE_FAST_THREADS) out[p] = labels[(size_t)i * HW + p];
+    return;
+  }
+  const unsigned full = (1u << nv) - 1u;
+  for (int p = threadIdx.x; p < HW; p += SIMPLE_FAST_THREADS) {
+    unsigned m = 0;
+    for (int idx = 0; idx < nv; ++idx) m |= (unsigned)(labels[((size_t)idx * T + (i - idx * step)) * HW + p] != 0) << idx;
+    msk[p] = (uint16_t)m;
+    est[p] = 0;
+  }
+  __syncthreads();
+  for (int lab = 1; lab >= 0; --lab) {
+    unsigned keep = full;
+    double wts[MV];
+    int inter[MV], csum[MV];
+    int conv;
+    {
+      // pass 0: unweighted majority (ties -> off), its size, its overlap with every candidate, and the
+      // candidate sizes
+      int acc[2 * MV + 1];
+#pragma unroll
+      for (int j = 0; j < 2 * MV + 1; ++j) acc[j] = 0;
+      for (int p = threadIdx.x; p < HW; p += SIMPLE_FAST_THREADS) {
+        const unsigned c = lab ? msk[p] : (~(unsigned)msk[p] & full);
+        const int on = __popc(c);
+        const unsigned e = on > nv - on;
+        est[p] = (uint8_t)((est[p] & 2u) | e);
+        acc[0] += e;
+#pragma unroll
+        for (int idx = 0; idx < MV; ++idx) {
+          const unsigned b = (c >> idx) & 1u;
+          acc[1 + idx] += b & e;
+          acc[1 + MV + idx] += b;
+        }
+      }
+      block_sum_vec<2 * MV + 1>(acc, red, tot);
+      conv = tot[0];
+#pragma unroll
+      for (int idx = 0; idx < MV; ++idx) {
+        inter[idx] = tot[1 + idx];
+        csum[idx] = tot[1 + MV + idx];
+        wts[idx] = 1.0;
+      }
+      __syncthreads();
+    }
+    for (int it = 0; it < 25; ++it) {
+      const double esum = (double)conv;
+      double mx = 0;
+#pragma unroll
+      for (int idx = 0; idx < MV; ++idx) {
+        if (idx >= nv || !(keep >> idx & 1u)) continue;
+        const double s2 = (double)csum[idx] + esum;
+        const double d = (s2 == 0) ? 1.0 : 2.0 * (double)inter[idx] / s2;
+        wts[idx] = (d + 1.0) * (d + 1.0);
+        mx = fmax(mx, wts[idx]);
+      }
+#pragma unroll
+      for (int idx = 0; idx < MV; ++idx)
+        if (idx < nv && (keep >> idx & 1u) && !(wts[idx] > 0.05 * mx)) keep &= ~(1u << idx);
+      int acc[MV + 1];
+#pragma unroll
+      for (int j = 0; j < MV + 1; ++j) acc[j] = 0;
+      for (int p = threadIdx.x; p < HW; p += SIMPLE_FAST_THREADS) {
+        const unsigned c = lab ? msk[p] : (~(unsigned)msk[p] & full);
+        double on = 0, off = 0;
+#pragma unroll
+        for (int idx = 0; idx < MV; ++idx) {
+          if (!(keep >> idx & 1u)) continue;  // keep has no bits at or above nv
+          if ((c >> idx) & 1u)
+            on += wts[idx];
+          else
+            off += wts[idx];
+        }
+        const unsigned e = on > off;
+        est[p] = (uint8_t)((est[p] & 2u) | e);
+        acc[0] += e;
+#pragma unroll
+        for (int idx = 0; idx < MV; ++idx) acc[1 + idx] += ((c >> idx) & 1u) & e;
+      }
+      block_sum_vec<MV + 1>(acc, red, tot);
+      const int nsum = tot[0];
+#pragma unroll
+      for (int idx = 0; idx < MV; ++idx) inter[idx] = tot[1 + idx];
+      __syncthreads();
+      const bool stop = fabs((double)conv - (double)nsum) < 25.0;
+      conv = nsum;
+      if (stop) break;
+    }
+    if (lab == 1)
+      for (int p = threadIdx.x; p < HW; p += SIMPLE_FAST_THREADS) est[p] = (uint8_t)((est[p] & 1u) << 1);
+    __syncthreads();
+  }
+  // label 1 where its estimate is on, then label 0 where its estimate is on (as the kernel above)
+  for (int p = threadIdx.x; p < HW; p += SIMPLE_FAST_THREADS) out[p] = (uint8_t)((est[p] & 2u) && !(est[p] & 1u));
+}
+
 // ---- warp ------------------------------------------------------------------------------------
 // torch.linspace(-1, 1, n) on the CPU: step = 2/(n-1); first half fma(step, i, -1), second half
 // fma(-step, n-1-i, 1) (the kernel is built with FMA contraction).
@@ -452,7 +593,20 @@ hipError_t launch_fuse_votes(const uint8_t* labels, int K, int T, int step, int 
                              hipStream_t s) {
   const int tout = T - (step - 1);
   if (method == 1) {
-    hipLaunchKernelGGL(fuse_simple_kernel, dim3(tout), dim3(SIMPLE_THREADS), HW, s, labels, K, T, step, HW, fused);
+    const size_t lds = 3 * (size_t)HW;
+    if (K <= SIMPLE_FAST_MAXV && lds <= 160 * 1024 && !getenv("CLASFV_SIMPLE_GENERIC")) {
+      static size_t attr = 0;
+      if (lds > 64 * 1024 && lds > attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)fuse_simple_fast_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = lds;
+      }
+      hipLaunchKernelGGL(fuse_simple_fast_kernel, dim3(tout), dim3(SIMPLE_FAST_THREADS), lds, s, labels, K, T, step, HW,
+                         fused);
+    } else {
+      hipLaunchKernelGGL(fuse_simple_kernel, dim3(tout), dim3(SIMPLE_THREADS), HW, s, labels, K, T, step, HW, fused);
+    }
   } else {
     dim3 grid(blocks_for(HW, 256, 64), tout);
     hipLaunchKernelGGL(fuse_majority_kernel, grid, dim3(256), 0, s, labels, K, T, step, HW, fused);

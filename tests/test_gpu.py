@@ -153,6 +153,45 @@ def test_pipeline_simple_vs_oracle(T, f, step):
     np.testing.assert_array_equal(out, ref)
 
 
+def _noisy_passes(K, T, step, H=40, W=48, seed=0):
+    """K pass label videos (pass k has T - k*step frames): a pulsing ellipse plus per-pass blotches, so
+    SIMPLE sees disagreeing candidates and iterates."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:H, 0:W]
+    passes = []
+    for k in range(K):
+        n = T - k * step
+        v = np.zeros((n, H, W), np.uint8)
+        for f in range(n):
+            t = f + k * step
+            a, b = 8 + 4 * np.sin(t / 5.0), 10 + 3 * np.cos(t / 7.0)
+            m = ((yy - H / 2) / a) ** 2 + ((xx - W / 2) / b) ** 2 <= 1
+            for _ in range(int(rng.integers(0, 4))):
+                cy, cx, r = rng.integers(0, H), rng.integers(0, W), rng.integers(2, 9)
+                m ^= (yy - cy) ** 2 + (xx - cx) ** 2 <= r * r
+            v[f] = m
+        passes.append(v)
+    return passes
+
+
+@pytest.mark.parametrize("K,T,step", [(2, 20, 1), (5, 40, 1), (10, 60, 1), (16, 70, 1), (6, 50, 3), (17, 60, 1)])
+def test_fuse_simple_kernels_vs_oracle(K, T, step, monkeypatch):
+    """SIMPLE fusion: the packed-mask kernel (K <= 16) and the generic kernel both equal the oracle's
+    restatement frame by frame (parity with LabelFusion itself unpinned)."""
+    from clasfv_amd import fuse_utils as FU
+    passes = _noisy_passes(K, T, step, seed=K * 100 + T)
+    labels = np.zeros((K, T) + passes[0].shape[1:], np.uint8)
+    for k, p in enumerate(passes):
+        labels[k, :p.shape[0]] = p
+    lab = torch.from_numpy(labels).cuda()
+    ref = fuse_ref.fuse_frames(passes, T, step, "simple")
+    fast = FU.fuse_votes(lab, step, "simple").cpu().numpy()
+    monkeypatch.setenv("CLASFV_SIMPLE_GENERIC", "1")
+    generic = FU.fuse_votes(lab, step, "simple").cpu().numpy()
+    np.testing.assert_array_equal(generic, ref)
+    np.testing.assert_array_equal(fast, ref)
+
+
 def test_pipeline_quirks():
     from clasfv_amd import fuse_utils as FU
     with pytest.raises(IndexError):
