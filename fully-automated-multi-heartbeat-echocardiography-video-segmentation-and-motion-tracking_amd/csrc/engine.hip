@@ -78,6 +78,7 @@ struct Conv {
   void* dw = nullptr;     // weights, dtype of the conv's input
   float* db = nullptr;    // folded-BN bias (fp32)
   float* dwino = nullptr;  // Winograd F(2x2,3x3) transformed weights (fp32 stride-1 1x3x3 convs)
+  float* dwinor = nullptr;  // Winograd F(2x4,3x3) transformed weights (the same convs, Cin <= 128)
   float* dwinot = nullptr;  // Winograd F(4,3)-in-time transformed weights (fp32 stride-1 3x1x1 convs)
 };
 
@@ -90,12 +91,17 @@ bool use_winot(const Conv& c, bool bf16) {
          c.st == 1 && c.cin_p % 8 == 0 && c.cout_p % 64 == 0;
 }
 
+bool use_winor(const Conv& c, bool bf16);
+
 bool use_wino(const Conv& c, bool bf16) {
   const char* e = getenv("CLASFV_WINOGRAD");
   if (e && e[0] == '0') return false;
   return !bf16 && (c.role == SP1 || c.role == SP2) && c.kt == 1 && c.kh == 3 && c.kw == 3 && c.sh == 1 &&
          c.sw == 1 && c.cin_p % 16 == 0 && c.cout_p % 48 == 0;
 }
+
+// F(2x4,3x3) weights only where conv_wino_r can run at 112x112 / 224x224 clips (layer1, layer2).
+bool use_winor(const Conv& c, bool bf16) { return use_wino(c, bf16) && c.cin_p <= 128; }
 
 // Channel padding, K extent and dtypes of one conv for the engine's compute dtype.
 void layout_conv(Conv& c, bool bf16) {
@@ -311,6 +317,14 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   p.stem = c.stem;
   p.in_bf16 = c.in_bf16;
   p.out_bf16 = c.out_bf16;
+  // F(2x4,3x3) is opt-in: 25 % fewer MFMAs than conv_wino_q but 1.5x its U operand traffic per
+  // output; measured slower on layer1 (2.80 vs 2.40 ms)
+  if (c.dwinor && getenv("CLASFV_WINO_R") && winor_supported(p)) {
+    p.w = c.dwinor;
+    HIP_TRY(launch_winor(p, s));
+    *kname = "conv_wino_r";
+    return CLASFV_OK;
+  }
   if (c.dwino) {
     p.w = c.dwino;
     const bool no_patch = getenv("CLASFV_NO_WINO_PATCH") != nullptr;  // A/B switch (tests)
@@ -424,6 +438,7 @@ int clasfv_destroy(clasfv_t h) {
     (void)hipFree(c.dw);
     (void)hipFree(c.db);
     (void)hipFree(c.dwino);
+    (void)hipFree(c.dwinor);
     (void)hipFree(c.dwinot);
   }
   for (auto& c : h->proj) (void)hipFree(c.dw);
@@ -485,9 +500,10 @@ int clasfv_finalize(clasfv_t h) {
     (void)hipFree(c.dw);
     (void)hipFree(c.db);
     (void)hipFree(c.dwino);
+    (void)hipFree(c.dwinor);
     (void)hipFree(c.dwinot);
     c.dw = c.db = nullptr;
-    c.dwino = c.dwinot = nullptr;
+    c.dwino = c.dwinor = c.dwinot = nullptr;
     bn_scale_shift(h, c.bn, c.cout, s, t);
     const auto& w = P(h, c.w + ".weight");
     const int taps = c.kt * c.kh * c.kw;
@@ -502,6 +518,11 @@ int clasfv_finalize(clasfv_t h) {
       std::vector<float> u((size_t)16 * c.cin_p * c.cout_p);
       wino_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, u.data());
       if ((rc = upload(u, &c.dwino))) return rc;
+      if (use_winor(c, bf16)) {
+        std::vector<float> ur((size_t)24 * c.cin_p * c.cout_p);
+        winor_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, ur.data());
+        if ((rc = upload(ur, &c.dwinor))) return rc;
+      }
     }
     if (use_winot(c, bf16)) {
       std::vector<double> wf((size_t)c.cout * cin * 3);

@@ -482,3 +482,24 @@ def test_kernel_variants_bitexact(model, monkeypatch, shape):
     monkeypatch.delenv("CLASFV_NO_WINO_PATCH")
     monkeypatch.delenv("CLASFV_NO_WINOT2")
     assert torch.equal(s_new, s_old) and torch.equal(m_new, m_old)
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112)])
+def test_wino_f2x4_matches_f2x2(model, monkeypatch, shape):
+    """conv_wino_r (F(2x4,3x3), opt-in with CLASFV_WINO_R where H, W % 8 == 0) against conv_wino_q
+    (F(2x2,3x3)): other Winograd products, same convolution -- logits within the forward bar, and
+    against the CPU oracle at the small shape."""
+    rng = np.random.default_rng(29)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    s_q, m_q = model(x)
+    monkeypatch.setenv("CLASFV_WINO_R", "1")
+    s_r, m_r = model(x)
+    monkeypatch.delenv("CLASFV_WINO_R")
+    assert not torch.equal(s_r, s_q)  # the F(2x4) kernel really ran
+    np.testing.assert_allclose(s_r.cpu().numpy(), s_q.cpu().numpy(), rtol=0, atol=2e-3)
+    np.testing.assert_allclose(m_r.cpu().numpy(), m_q.cpu().numpy(), rtol=0, atol=1e-5)
+    if shape[2] <= 16:
+        from oracle import r2plus1d_ref as R
+        import clasfv_amd.weights as W
+        rs, rm = R.forward(W.synthetic_state_dict(W.DEFAULT_SEED), x.cpu().numpy())
+        np.testing.assert_allclose(s_r.cpu().numpy(), rs.numpy(), rtol=0, atol=3e-3)

@@ -15,6 +15,7 @@
 hipError_t launch_wino_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko);
+hipError_t launch_winor(const ConvParams& p, hipStream_t s);
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
 
 // decoder: N clips of T x H x W, taps at (T, H/2, W/2), (T/2, H/4, W/4), (T/4, H/8), (T/8, H/16)
@@ -60,8 +61,8 @@ int main(int argc, char** argv) {
   std::vector<int> kos;
   for (int i = 9; i < argc; ++i) kos.push_back(atoi(argv[i]));
   if (kos.empty()) kos.push_back(0);
-  const bool winoq = !strcmp(kind, "winoq");
-  const bool wino = !strcmp(kind, "wino") || winoq, winot = !strcmp(kind, "winot");
+  const bool winoq = !strcmp(kind, "winoq"), winor = !strcmp(kind, "winor");
+  const bool wino = !strcmp(kind, "wino") || winoq || winor, winot = !strcmp(kind, "winot");
   const bool sp = wino || !strcmp(kind, "sp"), tp = winot || !strcmp(kind, "tp");
   ConvParams p;
   memset(&p, 0, sizeof(p));
@@ -81,7 +82,7 @@ int main(int argc, char** argv) {
   p.relu = 1;
   const size_t nx = (size_t)N * T * H * W * Cin, ny = (size_t)p.M * Cout;
   p.x = dev_random(nx, 0.f, 1.f, 1);
-  const size_t nw = wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
+  const size_t nw = winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
   p.w = dev_random(nw, -0.05f, 0.05f, 2);
   p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
   p.res = getenv("CB_NORES") ? nullptr : dev_random(ny, 0.f, 1.f, 4);
@@ -97,7 +98,8 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   auto launch = [&](int ko) {
-    if (winoq) CK(launch_winoq_ko(p, s, ko));
+    if (winor) CK(launch_winor(p, s));
+    else if (winoq) CK(launch_winoq_ko(p, s, ko));
     else if (wino) CK(launch_wino_ko(p, s, ko));
     else if (winot) CK(launch_winot_ko(p, s, ko));
     else {
