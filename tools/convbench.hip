@@ -15,7 +15,7 @@
 hipError_t launch_wino_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko);
-hipError_t launch_winor(const ConvParams& p, hipStream_t s);
+hipError_t launch_winor_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
 
 // decoder: N clips of T x H x W, taps at (T, H/2, W/2), (T/2, H/4, W/4), (T/4, H/8), (T/8, H/16)
@@ -98,7 +98,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   auto launch = [&](int ko) {
-    if (winor) CK(launch_winor(p, s));
+    if (winor) CK(launch_winor_ko(p, s, ko));
     else if (winoq) CK(launch_winoq_ko(p, s, ko));
     else if (wino) CK(launch_wino_ko(p, s, ko));
     else if (winot) CK(launch_winot_ko(p, s, ko));
