@@ -104,7 +104,7 @@ int main(int argc, char** argv) {
     else if (winot) CK(launch_winot_ko(p, s, ko));
     else {
       int mt, bn;
-      conv_pick_tile(p.M, Cout, 0, &mt, &bn);
+      conv_pick_tile(p.M, Cout, getenv("CB_NT") ? atoi(getenv("CB_NT")) : 0, &mt, &bn);
       CK(launch_conv(p, mt, bn, s));
     }
   };
