@@ -54,10 +54,10 @@ bool wino_supported(const ConvParams& p);
 hipError_t launch_wino(const ConvParams& p, hipStream_t s);
 // U[cin_p/8][4][cout_p][4][4][2] from folded weights w[cout][cin][3][3] (double).
 void wino_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
-// Patch-tiled Winograd F(2x2,3x3) for Ho, Wo % 8 == 0 (winograd2.hip); p.w = conv_wino's U.
+// Patch-tiled Winograd F(2x2,3x3) for Ho, Wo % 4 == 0 (winograd2.hip); p.w = conv_wino's U.
 bool winoq_supported(const ConvParams& p);
 hipError_t launch_winoq(const ConvParams& p, hipStream_t s);
-// Patch-tiled Winograd F(2x4,3x3) (winograd3.hip), same support as conv_wino_q; p.w = U below.
+// Patch-tiled Winograd F(2x4,3x3) (winograd3.hip), Ho, Wo % 8 == 0; p.w = U below.
 bool winor_supported(const ConvParams& p);
 hipError_t launch_winor(const ConvParams& p, hipStream_t s);
 // U[cin_p/8][4][cout_p][4][6][2] from folded weights w[cout][cin][3][3] (double).

@@ -8,7 +8,10 @@
 //  * the transform of chunk k+1 is split around the MFMAs of chunk k: its LDS reads are issued
 //    before them and its arithmetic and V stores are placed in the MFMA issue gaps
 //    (sched_group_barrier), so the matrix pipe no longer idles while a wave transforms.
-// Layer1 (30 clips, 64->144): 2.89 -> 2.61 ms (tools/convbench.sh). Requires Ho, Wo % 8 == 0.
+// Layer1 (30 clips, 64->144): 2.89 -> 2.61 ms (tools/convbench.sh). Maps with Ho, Wo % 8 == 0 use
+// 8x8-pixel patches (PT = 4 tiles per side); maps with Ho, Wo % 4 == 0 (layer2 at 112x112 clips:
+// 28x28) use 4x4-pixel patches (PT = 2: 8 patches of 6x6 input pixels per block, 1.78x fewer raw
+// bytes than per-tile windows; layer2 128->288: conv_wino 1.32 -> 1.18 ms).
 #include "common.h"
 
 namespace {
@@ -35,16 +38,36 @@ __device__ inline void dma16(const void* src, void* lds_dst) {
 // the same as the loads (KO 128), and loading chunk 0's U every chunk (L1-resident, KO 64) is no
 // faster: the U fetch is not a bottleneck; the MFMA issue stream itself is (SQ_VALU_MFMA_BUSY 57 %).
 constexpr int Q_BT = 32;
-constexpr int Q_RAW = 8 * 1024;       // 8 DMA wave-instructions (400 slots used)
 constexpr int Q_V = 16 * Q_BT * 32;   // 16 KB
-constexpr int Q_LDS = 3 * Q_RAW + 3 * Q_V;  // 72 KB: 2 blocks per CU
 
-template <int NCH, int KO = 0>
+// Patch geometry for PT tiles per patch side: PT = 4 (8x8-pixel outputs, 10x10 input; H, W % 8 == 0)
+// or PT = 2 (4x4 outputs, 6x6 input: 28x28 maps). A block always holds 32 tiles.
+template <int PT>
+struct QPatch {
+  static constexpr int SIDE = 2 * PT + 2;                 // input patch side (pixels)
+  static constexpr int PIX = SIDE * SIDE;
+  static constexpr int PPB = Q_BT / (PT * PT);            // patches per block
+  static constexpr int SLOTS = PPB * PIX * 2;             // 16-B DMA slots per chunk (8 channels)
+  static constexpr int DPW = ((SLOTS + 63) / 64 + 3) / 4;  // DMAs per wave per chunk
+  // raw stage = all 4*DPW wave-instructions when that still fits 2 blocks per CU, otherwise only the
+  // ones carrying data, the rest landing in a 1 KB sink
+  static constexpr bool FULL = 3 * (4 * DPW * 1024) + 3 * Q_V <= 80 * 1024;
+  static constexpr int NINSTR = FULL ? 4 * DPW : (SLOTS + 63) / 64;
+  static constexpr int RAW = NINSTR * 1024;               // raw stage bytes
+  static constexpr int LDS = 3 * RAW + 3 * Q_V + (FULL ? 0 : 1024);
+};
+static_assert(QPatch<4>::LDS == 72 * 1024 && QPatch<4>::DPW == 2, "PT = 4 layout");
+static_assert(QPatch<2>::DPW == 3 && QPatch<2>::LDS <= 80 * 1024, "PT = 2 layout: 2 blocks per CU");
+
+template <int NCH, int KO = 0, int PT = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino_q(ConvParams p, int n_co,
                                                                                              int n_patches) {
-  __shared__ __align__(16) char smem[Q_LDS];
+  using G = QPatch<PT>;
+  constexpr int Q_RAW = G::RAW, DPW = G::DPW;
+  __shared__ __align__(16) char smem[G::LDS];
   char* raw = smem;
   char* vbuf = smem + 3 * Q_RAW;
+  char* sink = smem + 3 * Q_RAW + 3 * Q_V;  // DMAs past NINSTR (PT = 2) land here
 
   const float* x = reinterpret_cast<const float*>(p.x);
   const float* U = reinterpret_cast<const float*>(p.w);
@@ -52,25 +75,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, l16 = lane & 15;
   const int blk = xcd_swizzle_p(blockIdx.x, gridDim.x);
-  const int pg0 = (blk / n_co) * 2, n0 = (blk % n_co) * 48;
+  const int pg0 = (blk / n_co) * G::PPB, n0 = (blk % n_co) * 48;
   const int H = p.Ho, W = p.Wo, C = p.Cin, CO = p.Cout;
-  const int PY = H >> 3, PX = W >> 3;
+  const int PY = H / (2 * PT), PX = W / (2 * PT);
   const int nchunk = NCH > 0 ? NCH : C >> 3;
 
-  // raw DMA: instruction j of this wave fills slots s = (wid + 4j)*64 + lane, s = pp*200 + pix*2 + half
-  int d_off[2];
+  // raw DMA: instruction j of this wave fills slots s = (wid + 4j)*64 + lane, s = pp*2*PIX + pix*2 + half
+  int d_off[DPW];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < DPW; ++j) {
     const int s = (wid + 4 * j) * 64 + lane;
     int off = -1;
-    if (s < 400) {
-      const int pp = s / 200, rem = s - pp * 200, pix = rem >> 1, half = rem & 1;
-      const int py = pix / 10, px = pix - py * 10;
+    if (s < G::SLOTS) {
+      const int pp = s / (2 * G::PIX), rem = s - pp * (2 * G::PIX), pix = rem >> 1, half = rem & 1;
+      const int py = pix / G::SIDE, px = pix - py * G::SIDE;
       const int gp = pg0 + pp;
       if (gp < n_patches) {
         const int f = gp / (PY * PX), r = gp - f * (PY * PX);
         const int pr = r / PX, pc = r - pr * PX;
-        const int yy = pr * 8 - 1 + py, xx = pc * 8 - 1 + px;
+        const int yy = pr * 2 * PT - 1 + py, xx = pc * 2 * PT - 1 + px;
         if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) off = ((f * H + yy) * W + xx) * C + half * 4;
       }
     }
@@ -79,11 +102,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   auto issue_raw = [&](int k, int stage) __attribute__((always_inline)) {
     if constexpr (KO & 2) return;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < DPW; ++j) {
       const void* src = (k < nchunk && d_off[j] >= 0) ? (const void*)(x + (size_t)d_off[j] + k * 8) : p.zero;
       if constexpr ((KO & 32) != 0)  // timing probe: same bytes, fully coalesced (wrong data)
         src = (const void*)(x + ((size_t)(blk & 4095) * 8 + (k & 7)) * 2048 + (size_t)((wid + 4 * j) * 64 + lane) * 4);
-      dma16(src, raw + stage * Q_RAW + (wid + 4 * j) * 1024);
+      // every wave issues DPW DMAs (wave-uniform vmcnt counts); those past NINSTR go to the sink
+      dma16(src, wid + 4 * j < G::NINSTR ? raw + stage * Q_RAW + (wid + 4 * j) * 1024 : sink);
     }
   };
   // U: lane (co = l16, q) of wave (e row) wid, n tile nt: 8 floats U[chunk][wid][co][q][j][s]
@@ -111,9 +135,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int h = 0; h < 2; ++h) u[nt][h] = *reinterpret_cast<const f32x4*>(b + (size_t)nt * 16 * 32 + h * 4);
   };
-  // transform thread = (tile tt = pp*16 + ly*4 + lx, channel cc)
+  // transform thread = (tile tt = pp*PT*PT + ly*PT + lx, channel cc)
   const int tt = tid >> 3, cc = tid & 7;
-  const int raw_off = (tt >> 4) * 800 + (2 * ((tt >> 2) & 3) * 10 + 2 * (tt & 3)) * 8 + cc;
+  const int raw_off = (tt / (PT * PT)) * G::PIX * 8 + (2 * ((tt / PT) % PT) * G::SIDE + 2 * (tt % PT)) * 8 + cc;
   const int v_off = (((tt & 15) * 4 + (cc >> 1)) * 2 + (tt >> 4)) * 2 + (cc & 1);  // V[e][tile&15][ci>>1][pp][ci&1]
   auto transform_read = [&](int rstage, float (&d)[16]) __attribute__((always_inline)) {
     if constexpr (KO & 1) {
@@ -125,7 +149,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) d[4 * r + c] = rb[(r * 10 + c) * 8];
+      for (int c = 0; c < 4; ++c) d[4 * r + c] = rb[(r * G::SIDE + c) * 8];
   };
   auto transform_write = [&](const float (&d)[16], int vstage) __attribute__((always_inline)) {
     if constexpr (KO & 1) return;
@@ -178,7 +202,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __builtin_amdgcn_sched_barrier(0);
   load_u(0, uu[0]);
   __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_waitcnt(0x0F70 | 10);  // vmcnt(10): raw(0) landed
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * DPW + 6));  // raw(0) landed (raw(1), raw(2), U(0) in flight)
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   {
@@ -186,7 +210,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     transform_read(0, d);
     transform_write(d, 0);
   }
-  __builtin_amdgcn_s_waitcnt(0x0F70 | 8);  // vmcnt(8): raw(1) landed
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (DPW + 6));  // raw(1) landed (raw(2), U(0) in flight)
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();  // every wave has read raw stage 0
   __builtin_amdgcn_sched_barrier(0);
@@ -207,8 +231,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
   auto step = [&](int k, f32x4 (&uc)[3][2], f32x4 (&un)[3][2], f32x4 (&ac)[4], f32x4 (&an)[4])
                   __attribute__((always_inline)) {
-    // vmcnt(8): raw(k+2), U(k) landed; lgkmcnt(0): own V stores and operand reads done
-    __builtin_amdgcn_s_waitcnt(0x0070 | 8);
+    // vmcnt(DPW + 6): raw(k+2), U(k) landed; lgkmcnt(0): own V stores and operand reads done
+    __builtin_amdgcn_s_waitcnt(0x0070 | (DPW + 6));
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -239,9 +263,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // DS read (8 transform, 4 operand)
       }
 #pragma unroll
-      for (int g = 0; g < 8; ++g) {
+      for (int g = 0; g < DPW + 6; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (2 LDS-DMAs, 6 U loads)
+        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (DPW LDS-DMAs, 6 U loads)
       }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
@@ -293,12 +317,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   for (int u = 0; u < UPT; ++u) {
     const int un = tid + 256 * u;
     const int tl = un / CQ, cq = un - tl * CQ;
-    const int gp = pg0 + (tl >> 4);
+    const int gp = pg0 + tl / (PT * PT);
     const bool live = un < UNITS && gp < n_patches;
     const int gpc = live ? gp : pg0;
     const int f = gpc / (PY * PX), r = gpc - f * (PY * PX);
     const int pr = r / PX, pc = r - pr * PX;
-    const int yy = pr * 8 + 2 * ((tl >> 2) & 3), xx = pc * 8 + 2 * (tl & 3);
+    const int yy = pr * 2 * PT + 2 * ((tl / PT) % PT), xx = pc * 2 * PT + 2 * (tl % PT);
     const int co = n0 + 4 * cq;
     u_o[u] = ((size_t)(f * H + yy) * W + xx) * CO + co;
     u_z[u] = tl * 48 + 4 * cq;
@@ -350,11 +374,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-template <int NCH, int KO = 0>
+template <int NCH, int KO = 0, int PT = 4>
 hipError_t launch_q(const ConvParams& p, hipStream_t s) {
-  const int n_patches = p.N * p.To * (p.Ho >> 3) * (p.Wo >> 3);
+  constexpr int PPB = QPatch<PT>::PPB;
+  const int n_patches = p.N * p.To * (p.Ho / (2 * PT)) * (p.Wo / (2 * PT));
   const int n_co = p.Cout / 48;
-  hipLaunchKernelGGL((conv_wino_q<NCH, KO>), dim3(((n_patches + 1) / 2) * n_co), dim3(256), 0, s, p, n_co, n_patches);
+  hipLaunchKernelGGL((conv_wino_q<NCH, KO, PT>), dim3(((n_patches + PPB - 1) / PPB) * n_co), dim3(256), 0, s, p, n_co,
+                     n_patches);
   return hipGetLastError();
 }
 
@@ -363,23 +389,31 @@ hipError_t launch_q(const ConvParams& p, hipStream_t s) {
 bool winoq_supported(const ConvParams& p) {
   return !p.in_bf16 && !p.out_bf16 && !p.stem && !p.x2 && p.KT == 1 && p.KH == 3 && p.KW == 3 && p.sh == 1 &&
          p.sw == 1 && p.st == 1 && p.ph == 1 && p.pw == 1 && p.pt == 0 && p.Cin % 8 == 0 && p.Cout % 48 == 0 &&
-         p.Ho == p.Hi && p.Wo == p.Wi && p.To == p.Ti && p.Ho % 8 == 0 && p.Wo % 8 == 0 &&
+         p.Ho == p.Hi && p.Wo == p.Wi && p.To == p.Ti && p.Ho % 4 == 0 && p.Wo % 4 == 0 &&
          (size_t)p.N * p.To * p.Ho * p.Wo * (p.Cin > p.Cout ? p.Cin : p.Cout) < ((size_t)1 << 31);
 }
 
 // p.w: conv_wino's U layout [Cin/8][4][Cout][4][4][2] (wino_transform_weights).
 hipError_t launch_winoq(const ConvParams& p, hipStream_t s) {
   if (!winoq_supported(p)) return hipErrorInvalidValue;
-  switch (p.Cin >> 3) {
-    case 8: return launch_q<8>(p, s);
-    case 16: return launch_q<16>(p, s);
-    default: return launch_q<0>(p, s);
+  if (p.Ho % 8 == 0 && p.Wo % 8 == 0) {  // 8x8-pixel patches
+    switch (p.Cin >> 3) {
+      case 8: return launch_q<8, 0, 4>(p, s);
+      case 16: return launch_q<16, 0, 4>(p, s);
+      default: return launch_q<0, 0, 4>(p, s);
+    }
+  }
+  switch (p.Cin >> 3) {  // 4x4-pixel patches (28x28 maps)
+    case 8: return launch_q<8, 0, 2>(p, s);
+    case 16: return launch_q<16, 0, 2>(p, s);
+    default: return launch_q<0, 0, 2>(p, s);
   }
 }
 
 #ifdef CLASFV_KNOCKOUTS
 hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko) {
-  if (p.Cin != 64) return hipErrorInvalidValue;
+  if (ko == 0) return launch_winoq(p, s);
+  if (p.Cin != 64 || p.Ho % 8 || p.Wo % 8) return hipErrorInvalidValue;
   switch (ko) {
     case 0: return launch_q<8, 0>(p, s);
     case 1: return launch_q<8, 1>(p, s);

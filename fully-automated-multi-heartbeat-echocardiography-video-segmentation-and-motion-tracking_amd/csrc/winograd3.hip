@@ -353,7 +353,7 @@ hipError_t launch_r(const ConvParams& p, hipStream_t s) {
 
 }  // namespace
 
-bool winor_supported(const ConvParams& p) { return winoq_supported(p); }
+bool winor_supported(const ConvParams& p) { return winoq_supported(p) && p.Ho % 8 == 0 && p.Wo % 8 == 0; }
 
 // p.w: U[Cin/8][4][Cout][4][6][2] (winor_transform_weights).
 hipError_t launch_winor(const ConvParams& p, hipStream_t s) {
