@@ -234,12 +234,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // vmcnt(DPW + 6): raw(k+2), U(k) landed; lgkmcnt(0): own V stores and operand reads done
     __builtin_amdgcn_s_waitcnt(0x0070 | (DPW + 6));
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((KO & 256) == 0) __builtin_amdgcn_s_barrier();  // KO 256: timing probe only
+    __builtin_amdgcn_sched_barrier(0);
+    // raw(k+4) LDS-DMAs before this chunk's LDS reads: issued after them, the compiler drains the
+    // reads (lgkmcnt(0)) in front of the DMA, which stalls the wave's MFMA stream
+    issue_raw(k + 4, (k + 1) % 3);
     __builtin_amdgcn_sched_barrier(0);
     read_a((k + 1) % 3, an);
     float d[16];  // raw(k+2) -> V((k+2)%3); branch-free (the last chunks transform unused fetches)
     transform_read((k + 2) % 3, d);
-    issue_raw(k + 4, (k + 1) % 3);
     load_u(k + 2, un);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -411,6 +414,19 @@ hipError_t launch_winoq(const ConvParams& p, hipStream_t s) {
 }
 
 #ifdef CLASFV_KNOCKOUTS
+// occupancy probe: the same kernel at one block per CU (80 KB of extra dynamic LDS)
+template <int KO>
+static hipError_t launch_q1(const ConvParams& p, hipStream_t s) {
+  const int n_patches = p.N * p.To * (p.Ho >> 3) * (p.Wo >> 3);
+  const int n_co = p.Cout / 48;
+  hipError_t e = hipFuncSetAttribute((const void*)conv_wino_q<8, KO, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     80 * 1024);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((conv_wino_q<8, KO, 4>), dim3(((n_patches + 1) / 2) * n_co), dim3(256), 80 * 1024, s, p, n_co,
+                     n_patches);
+  return hipGetLastError();
+}
+
 hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko) {
   if (ko == 0) return launch_winoq(p, s);
   if (p.Cin != 64 || p.Ho % 8 || p.Wo % 8) return hipErrorInvalidValue;
@@ -427,6 +443,12 @@ hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 32: return launch_q<8, 32>(p, s);
     case 64: return launch_q<8, 64>(p, s);
     case 128: return launch_q<8, 128>(p, s);
+    case 512: return launch_q1<0>(p, s);
+    case 513: return launch_q1<1>(p, s);
+    case 514: return launch_q1<2>(p, s);
+    case 520: return launch_q1<8>(p, s);
+    case 768: return launch_q1<256>(p, s);
+    case 256: return launch_q<8, 256>(p, s);
   }
   return hipErrorInvalidValue;
 }
