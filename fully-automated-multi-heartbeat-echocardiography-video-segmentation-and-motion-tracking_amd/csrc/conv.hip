@@ -350,6 +350,20 @@ hipError_t launch_typed(const ConvParams& p, int bn, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
+// bf16 with BM = 256 (4 waves x 64 rows): a K step moves (16 + NT) KiB for 16*NT MFMAs per wave
+// instead of (8 + NT) KiB for 8*NT -- the direct bf16 convs are bound by the global->LDS bytes.
+hipError_t launch_bf16_m4(const ConvParams& p, int bn, hipStream_t s) {
+  switch (bn) {
+    case 48: return launch_dma<__bf16, 4, 3, 3>(p, s);
+    case 64: return launch_dma<__bf16, 4, 4, 3>(p, s);
+    case 80: return launch_dma<__bf16, 4, 5, 3>(p, s);
+    case 96: return launch_dma<__bf16, 4, 6, 3>(p, s);
+    case 128: return launch_dma<__bf16, 4, 8, 3>(p, s);
+    case 144: return launch_dma<__bf16, 4, 9, 3>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
 }  // namespace
 
 // Tile choice: BM = 128 (mt = 2) and the widest N tile (16*NT, NT <= 9) dividing Cout.
@@ -371,6 +385,7 @@ void conv_pick_tile(int M, int cout_p, int force_nt, int* mt_out, int* bn_out) {
 }
 
 hipError_t launch_conv(const ConvParams& p, int mt, int bn, hipStream_t s) {
+  if (mt == 4 && p.in_bf16 && !p.stem) return launch_bf16_m4(p, bn, s);
   if (mt != 2) return hipErrorInvalidValue;
   if (p.stem) {  // fp32 input with 4 channels (3 + zero pad)
     if (bn == 48) return launch_stem<3>(p, s);

@@ -349,10 +349,18 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
     }
     p.w = c.dw;
   }
+  const bool no_patch_bf16 = getenv("CLASFV_NO_PATCH_BF16") != nullptr;  // A/B switch (tests)
+  if (!no_patch_bf16 && patch_bf16_supported(p)) {
+    HIP_TRY(launch_patch_bf16(p, s));
+    *kname = "conv_patch";
+    return CLASFV_OK;
+  }
   int mt = 2, bn = c.cout_p;  // stem: one N tile (48 fp32 / 64 bf16 channels)
   if (!c.stem) {
     static const int force_nt = getenv("CLASFV_CONV_NT") ? atoi(getenv("CLASFV_CONV_NT")) : 0;
     conv_pick_tile(p.M, c.cout_p, force_nt, &mt, &bn);
+    static const int force_mt = getenv("CLASFV_CONV_MT") ? atoi(getenv("CLASFV_CONV_MT")) : 0;
+    if (force_mt == 4 && p.in_bf16) mt = 4;  // A/B switch
   }
   HIP_TRY(launch_conv(p, mt, bn, s));
   *kname = c.stem ? "conv_stem_f32" : "conv_dma";

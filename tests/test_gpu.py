@@ -447,6 +447,38 @@ def test_forward_bf16_vs_reference_golden_config4_tolerance(model):
 
 
 @pytest.mark.parametrize("shape", [(1, 3, 32, 112, 112), (2, 3, 16, 64, 48)])
+def test_bf16_patch_conv_matches_direct_conv(model, monkeypatch, shape):
+    """bf16 stride-1 1x3x3 convs: the patch-staged kernel (conv_patch.hip, chunk-major K order)
+    against the direct LDS-DMA kernel (CLASFV_NO_PATCH_BF16=1, tap-major K order). The two sum the
+    same bf16 products in different fp32 orders, so bf16 activations may round differently: the
+    patch path's error against the fp32 forward must be no larger than the direct path's, and on the
+    echo-style clip both stay within the config[4] bar (Dice delta <= 1e-2). The (2,3,16,64,48) case
+    has ragged maps (layer3 16x12, layer4 8x6: masked tiles)."""
+    import clasfv_amd.synthetic as S
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    if shape[2:] == (32, 112, 112):
+        v = fuse_ref.zeroone_normalizer(S.echo_video(64, seed=3))
+        x = torch.from_numpy(np.ascontiguousarray(v[None, :, 10:42]))
+    else:
+        x = torch.from_numpy(np.random.default_rng(23).uniform(0, 1, shape).astype(np.float32))
+    s32, _ = model(x)
+    m16 = R2plus1D_18_MotionNet(pretrained=False, dtype="bf16")
+    s_p, m_p = m16(x)
+    monkeypatch.setenv("CLASFV_NO_PATCH_BF16", "1")
+    s_d, m_d = m16(x)
+    monkeypatch.delenv("CLASFV_NO_PATCH_BF16")
+    assert torch.isfinite(s_p).all() and torch.isfinite(m_p).all()
+    e_p, e_d = (s_p - s32).abs(), (s_d - s32).abs()
+    assert float(e_p.median()) <= 1.5 * float(e_d.median()) + 1e-3, (float(e_p.median()), float(e_d.median()))
+    assert float(e_p.max()) <= 2 * float(e_d.max()) + 1e-2, (float(e_p.max()), float(e_d.max()))
+    lab32 = (s32[:, 1] > s32[:, 0]).cpu().numpy().ravel()
+    lab_p = (s_p[:, 1] > s_p[:, 0]).cpu().numpy().ravel()
+    assert (lab_p == lab32).mean() >= 0.99
+    if shape[2:] == (32, 112, 112):
+        assert lab32.sum() > 1000 and dice_delta(lab_p, lab32) <= 1e-2
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 32, 112, 112), (2, 3, 16, 64, 48)])
 def test_winograd_path_matches_direct_conv(model, monkeypatch, shape):
     """The fused Winograd F(2x2,3x3) kernel (default for stride-1 1x3x3 fp32 convs) against the
     direct implicit-GEMM kernel (CLASFV_WINOGRAD=0), and both against the CPU oracle."""

@@ -43,6 +43,22 @@ static void* dev_random(size_t n, float lo, float hi, unsigned seed) {
   return d;
 }
 
+static void* to_bf16_dev(size_t n, float lo, float hi, unsigned seed) {
+  std::vector<uint16_t> h(n);
+  unsigned s = seed * 2654435761u + 1;
+  for (size_t i = 0; i < n; ++i) {
+    s = s * 1664525u + 1013904223u;
+    const float f = lo + (hi - lo) * ((s >> 8) * (1.0f / 16777216.0f));
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    h[i] = (uint16_t)((u + 0x7fff + ((u >> 16) & 1)) >> 16);
+  }
+  void* d;
+  CK(hipMalloc(&d, n * 2));
+  CK(hipMemcpy(d, h.data(), n * 2, hipMemcpyHostToDevice));
+  return d;
+}
+
 int main(int argc, char** argv) {
   if (argc < 8) {
     fprintf(stderr, "usage: convbench KIND N T H W CIN COUT [ITERS] [KO...]\n");
@@ -63,7 +79,8 @@ int main(int argc, char** argv) {
   if (kos.empty()) kos.push_back(0);
   const bool winoq = !strcmp(kind, "winoq"), winor = !strcmp(kind, "winor");
   const bool wino = !strcmp(kind, "wino") || winoq || winor, winot = !strcmp(kind, "winot");
-  const bool sp = wino || !strcmp(kind, "sp"), tp = winot || !strcmp(kind, "tp");
+  const bool spp = !strcmp(kind, "spp");  // bf16 patch-staged 1x3x3 (conv_patch.hip)
+  const bool sp = wino || spp || !strcmp(kind, "sp"), tp = winot || !strcmp(kind, "tp");
   ConvParams p;
   memset(&p, 0, sizeof(p));
   p.N = N, p.Ti = T, p.Hi = H, p.Wi = W, p.Cin = Cin;
@@ -76,16 +93,19 @@ int main(int argc, char** argv) {
     if (sp) p.sh = p.sw = 2, p.Ho = (H - 1) / 2 + 1, p.Wo = (W - 1) / 2 + 1;
     if (tp) p.st = 2, p.To = (T - 1) / 2 + 1;
   }
+  // CB_BF16=1: bf16 activations/weights/outputs (direct convs only), K step 32
+  const bool bf = (getenv("CB_BF16") || spp) && !wino && !winot;
+  p.in_bf16 = p.out_bf16 = bf;
   p.K = p.KT * p.KH * p.KW * Cin;
-  p.Kp = (p.K + 15) / 16 * 16;
+  p.Kp = bf ? (p.K + 31) / 32 * 32 : (p.K + 15) / 16 * 16;
   p.M = N * p.To * p.Ho * p.Wo;
   p.relu = 1;
   const size_t nx = (size_t)N * T * H * W * Cin, ny = (size_t)p.M * Cout;
-  p.x = dev_random(nx, 0.f, 1.f, 1);
+  p.x = bf ? to_bf16_dev(nx, 0.f, 1.f, 1) : dev_random(nx, 0.f, 1.f, 1);
   const size_t nw = winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
-  p.w = dev_random(nw, -0.05f, 0.05f, 2);
+  p.w = bf ? to_bf16_dev(nw, -0.05f, 0.05f, 2) : dev_random(nw, -0.05f, 0.05f, 2);
   p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
-  p.res = getenv("CB_NORES") ? nullptr : dev_random(ny, 0.f, 1.f, 4);
+  p.res = getenv("CB_NORES") ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
   CK(hipMalloc(&p.y, ny * 4));
   void* z;
   CK(hipMalloc(&z, 256));
@@ -102,9 +122,11 @@ int main(int argc, char** argv) {
     else if (winoq) CK(launch_winoq_ko(p, s, ko));
     else if (wino) CK(launch_wino_ko(p, s, ko));
     else if (winot) CK(launch_winot_ko(p, s, ko));
+    else if (spp) CK(launch_patch_bf16(p, s));
     else {
       int mt, bn;
       conv_pick_tile(p.M, Cout, getenv("CB_NT") ? atoi(getenv("CB_NT")) : 0, &mt, &bn);
+      if (getenv("CB_MT")) mt = atoi(getenv("CB_MT"));
       CK(launch_conv(p, mt, bn, s));
     }
   };
@@ -124,7 +146,7 @@ int main(int argc, char** argv) {
       if (ms < best[v]) best[v] = ms;
     }
   for (size_t v = 0; v < kos.size(); ++v)
-    printf("%s%-6s N=%d T=%d H=%d W=%d Cin=%d Cout=%d ko=%-3d  %8.3f ms  %7.1f TF(alg)\n", p.res ? "res   " : "nores ",
+    printf("%s%s%-6s N=%d T=%d H=%d W=%d Cin=%d Cout=%d ko=%-3d  %8.3f ms  %7.1f TF(alg)\n", p.res ? "res   " : "nores ", bf ? "bf16 " : "",
            kind, N, T, H, W, Cin, Cout, kos[v], best[v], gflop / best[v]);
   return 0;
 }
