@@ -26,17 +26,21 @@ SIGNATURES = {
     "clasfv_get_compute_dtype": (c_int, [_P]),
     "clasfv_set_kernel_timing": (c_int, [_P, c_int]),
     "clasfv_kernel_timing": (c_int, [_P, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int),
-                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double)]),
     "clasfv_build_clips": (c_int, [_P, c_int, c_int, c_int, _P, c_int, c_int, _P, _P]),
     "clasfv_pass_labels": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, _P]),
+    "clasfv_pass_labels_margin": (c_int, [_P, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P, _P]),
+    "clasfv_logit_margin": (c_int, [_P, c_int, c_int, c_int, _P, _P]),
     "clasfv_fuse_votes": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, c_int, _P, _P]),
     "clasfv_warp": (c_int, [_P, c_int, c_int, c_int, c_int, _P, c_int64, c_int64, _P, _P]),
-    "clasfv_zeroone_normalize": (c_int, [_P, c_int64, _P]),
+    "clasfv_zeroone_workspace_bytes": (c_int64, []),
+    "clasfv_zeroone_normalize": (c_int, [_P, c_int64, _P, _P]),
     "clasfv_warp_backward": (c_int, [_P, _P, c_int, c_int, c_int, c_int, _P, c_int64, c_int64, _P, _P, _P]),
     "clasfv_preprocess_video": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, _P, _P]),
 }
 
-FUSE_MAJORITY, FUSE_SIMPLE = 0, 1
+FUSE_MAJORITY, FUSE_SIMPLE, FUSE_STAPLE = 0, 1, 2
 DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
 _lib = None
 
@@ -69,9 +73,11 @@ def check(rc, what=""):
     return rc
 
 
-def stream_ptr(stream=None):
+def stream_ptr(stream=None, device=None):
+    """hipStream_t of ``stream``, else the current stream of ``device`` (a tensor's device: the
+    stream the caller's work on that device is ordered on), else of the current device."""
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
+    s = stream if stream is not None else torch.cuda.current_stream(device)
     return ctypes.c_void_p(s.cuda_stream)
 
 

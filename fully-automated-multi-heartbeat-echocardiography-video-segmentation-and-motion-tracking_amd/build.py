@@ -39,17 +39,35 @@ def up_to_date():
 
 
 def build(force=False, verbose=False):
-    """Compile the engine. Returns the library path."""
+    """Compile the engine. Returns the library path. Each source is compiled to an object in
+    parallel (every kernel is launched from its own translation unit, so no relocatable device
+    code is needed), then the objects are linked into one shared library."""
     if not force and up_to_date():
         return LIB_PATH
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = os.path.join(PKG_DIR, "build_obj")
+    os.makedirs(objdir, exist_ok=True)
+    hipcc = _hipcc()
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", INCLUDE]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src} ({r.returncode}):\n{r.stderr[-6000:]}")
+        return obj
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
     tmp = LIB_PATH + ".tmp"
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", INCLUDE,
-           "-o", tmp] + [os.path.join(CSRC, f) for f in SOURCES]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)
+    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs,
+                       capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-6000:]}")
+        raise RuntimeError(f"link failed ({r.returncode}):\n{r.stderr[-6000:]}")
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
 

@@ -144,7 +144,6 @@ struct clasfv_engine {
   // workspace arena
   char* arena = nullptr;
   size_t arena_bytes = 0;
-  float* part = nullptr;  // normaliser partials
   float* zero = nullptr;  // 256 zero bytes for padding taps
   // per-kernel HIP-event timing of clasfv_forward (clasfv_set_kernel_timing)
   bool ktime = false;
@@ -152,7 +151,8 @@ struct clasfv_engine {
   int nev = 0;
   struct Rec {
     const char* name;
-    double gflop;
+    double gflop;   // algorithmic (direct-convolution MACs x 2, unpadded channels)
+    double xgflop;  // MFMA work the launch executes (Winograd-domain products, padded channels/tiles)
     int e0, e1;
   };
   std::vector<Rec> recs;
@@ -291,6 +291,23 @@ double conv_gflop(const Conv& c, const Shape5& out) {
   return 2.0 * m * c.cout * (double)(c.cin + c.cin2) * c.kt * c.kh * c.kw * 1e-9;
 }
 
+// MFMA work one launch of kernel `kname` executes for conv c (2 FLOP per multiply-add issued to
+// the matrix cores, padded channels and partial tiles included): Winograd F(2x2,3x3) issues 16
+// products per 2x2 output tile and (input, output) channel pair instead of 36, F(2x4,3x3) 24 per
+// 2x4 tile instead of 72, F(4,3) in time 6 per 4 frames instead of 12; the implicit GEMMs issue
+// ceil(M / BM) * BM rows x cout_p x Kp.
+double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
+  const double nt = (double)out.n * out.t;
+  const double cc = (double)c.cin_p * c.cout_p;
+  if (!strcmp(kname, "conv_wino_q") || !strcmp(kname, "conv_wino"))
+    return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 1) / 2) * 16.0 * cc * 1e-9;
+  if (!strcmp(kname, "conv_wino_r")) return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 3) / 4) * 24.0 * cc * 1e-9;
+  if (!strcmp(kname, "conv_winot")) return 2.0 * out.n * (out.t / 4) * (double)out.h * out.w * 6.0 * cc * 1e-9;
+  const double m = (double)out.n * out.t * out.h * out.w;
+  const double bm = !strcmp(kname, "conv_patch") ? 1.0 : 128.0;
+  return 2.0 * (ceil(m / bm) * bm) * c.cout_p * (double)c.Kp * 1e-9;
+}
+
 int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
              hipStream_t s, const void* zero_block, const void* x2, const char** kname) {
   out.n = in.n;
@@ -420,6 +437,25 @@ int tick(clasfv_engine* h, hipStream_t s) {
 
 float tap_scale(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
 
+// Makes the handle's device current for the scope of an ABI call and restores the caller's.
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+#define DEVICE_GUARD(dev)                                                                       \
+  DeviceGuard _guard(dev);                                                                      \
+  if (_guard.err != hipSuccess)                                                                 \
+    return fail(CLASFV_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(_guard.err))
+
 }  // namespace
 
 extern "C" {
@@ -441,7 +477,7 @@ int clasfv_create(int device, clasfv_t* out) {
 
 int clasfv_destroy(clasfv_t h) {
   if (!h) return CLASFV_OK;
-  (void)hipSetDevice(h->device);
+  DeviceGuard guard(h->device);
   for (auto& c : h->convs) {
     (void)hipFree(c.dw);
     (void)hipFree(c.db);
@@ -456,7 +492,6 @@ int clasfv_destroy(clasfv_t h) {
   (void)hipFree(h->wh);
   (void)hipFree(h->bh);
   (void)hipFree(h->arena);
-  (void)hipFree(h->part);
   (void)hipFree(h->zero);
   for (auto e : h->evs) (void)hipEventDestroy(e);
   delete h;
@@ -499,7 +534,7 @@ int clasfv_finalize(clasfv_t h) {
   for (const auto& p : h->params)
     if (!p.loaded && p.name.find(".fc.") == std::string::npos)
       return fail(CLASFV_ENOTREADY, "parameter not loaded: " + p.name);
-  HIP_TRY(hipSetDevice(h->device));
+  DEVICE_GUARD(h->device);
   const bool bf16 = h->dtype == CLASFV_DTYPE_BF16;
   for (auto& c : h->convs) layout_conv(c, bf16);
   for (auto& c : h->proj) layout_conv(c, bf16);
@@ -625,7 +660,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
     return fail(CLASFV_EBADSHAPE, "shape must satisfy T % 8 == 0, H % 16 == 0, W % 16 == 0 (got T=" +
                                       std::to_string(T) + " H=" + std::to_string(H) + " W=" + std::to_string(W) + ")");
   hipStream_t s = (hipStream_t)stream;
-  HIP_TRY(hipSetDevice(h->device));
+  DEVICE_GUARD(h->device);
   Layout L;
   make_layout(N, T, H, W, L);
   if (L.total > h->arena_bytes) {
@@ -639,22 +674,22 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   }
   auto buf = [&](int b) { return reinterpret_cast<void*>(h->arena + L.off[b]); };
   int last_ev = h->ktime ? tick(h, s) : -1;
-  auto timed = [&](const char* name, double gflop) {
+  auto timed = [&](const char* name, double gflop, double xgflop) {
     if (last_ev < 0) return;
     const int e = tick(h, s);
-    if (e >= 0) h->recs.push_back({name, gflop, last_ev, e});
+    if (e >= 0) h->recs.push_back({name, gflop, xgflop, last_ev, e});
     last_ev = e;
   };
   auto run = [&](const Conv& c, const void* xin, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
                  const void* x2 = nullptr) {
     const char* kname = "";
     int rc_ = run_conv(c, xin, in, y, out, res, relu, s, h->zero, x2, &kname);
-    if (!rc_) timed(kname, conv_gflop(c, out));
+    if (!rc_) timed(kname, conv_gflop(c, out), conv_exec_gflop(c, out, kname));
     return rc_;
   };
 
   HIP_TRY(launch_pack_input(x, reinterpret_cast<float*>(buf(XIN)), N, T, H * W, s));
-  timed("pack_input_kernel", 0.0);
+  timed("pack_input_kernel", 0.0, 0.0);
   Shape5 sx{N, T, H, W, 4}, s0, sx0;
   int rc;
   size_t ci = 0;
@@ -719,7 +754,9 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   d.mot = mot;
   d.N = N, d.T = T, d.H = H, d.W = W;
   HIP_TRY(launch_decoder(d, s));
-  timed("decoder_kernel", 2.0 * N * (double)T * H * W * (64 * 64 + 64 * 6) * 1e-9);
+  // comb_2 (64x64) and the heads (6 useful of the 16 rows of their MFMA tile) per output voxel
+  timed("decoder_kernel", 2.0 * N * (double)T * H * W * (64 * 64 + 64 * 6) * 1e-9,
+        2.0 * N * (double)T * H * W * (64 * 64 + 64 * 16) * 1e-9);
   return CLASFV_OK;
 }
 
@@ -731,8 +768,10 @@ int clasfv_set_kernel_timing(clasfv_t h, int enable) {
   return CLASFV_OK;
 }
 
-int clasfv_kernel_timing(clasfv_t h, int cap, const char** names, int* launches, double* ms, double* gflop) {
-  if (!h || cap < 0 || (cap > 0 && (!names || !launches || !ms || !gflop))) return fail(CLASFV_EINVAL, "bad argument");
+int clasfv_kernel_timing(clasfv_t h, int cap, const char** names, int* launches, double* ms, double* gflop,
+                         double* xgflop) {
+  if (!h || cap < 0 || (cap > 0 && (!names || !launches || !ms || !gflop || !xgflop)))
+    return fail(CLASFV_EINVAL, "bad argument");
   if (h->nev > 0) HIP_TRY(hipEventSynchronize(h->evs[h->nev - 1]));
   int n = 0;
   for (const auto& r : h->recs) {
@@ -744,12 +783,13 @@ int clasfv_kernel_timing(clasfv_t h, int cap, const char** names, int* launches,
       if (n == cap) return fail(CLASFV_EINVAL, "kernel timing: cap too small");
       names[n] = r.name;
       launches[n] = 0;
-      ms[n] = gflop[n] = 0.0;
+      ms[n] = gflop[n] = xgflop[n] = 0.0;
       ++n;
     }
     launches[i] += 1;
     ms[i] += t;
     gflop[i] += r.gflop;
+    xgflop[i] += r.xgflop;
   }
   h->recs.clear();
   h->nev = 0;
@@ -768,15 +808,31 @@ int clasfv_pass_labels(const float* logits, int K, const int32_t* clip0, int T, 
                        uint8_t* labels, void* stream) {
   if (!logits || !clip0 || !labels || K < 1 || K > CLASFV_MAX_PASSES || T < 1 || step < 1)
     return fail(CLASFV_EINVAL, "bad argument (K must be in [1, 64])");
-  HIP_TRY(launch_pass_labels(logits, K, clip0, T, step, H * W, interp, labels, (hipStream_t)stream));
+  HIP_TRY(launch_pass_labels(logits, K, clip0, T, step, H * W, interp, 0, labels, (hipStream_t)stream));
+  return CLASFV_OK;
+}
+
+int clasfv_pass_labels_margin(const float* margin, int K, const int32_t* clip0, int T, int step, int H, int W,
+                              int interp, uint8_t* labels, void* stream) {
+  if (!margin || !clip0 || !labels || K < 1 || K > CLASFV_MAX_PASSES || T < 1 || step < 1)
+    return fail(CLASFV_EINVAL, "bad argument (K must be in [1, 64])");
+  HIP_TRY(launch_pass_labels(margin, K, clip0, T, step, H * W, interp, 1, labels, (hipStream_t)stream));
+  return CLASFV_OK;
+}
+
+int clasfv_logit_margin(const float* logits, int n, int H, int W, float* margin, void* stream) {
+  if (!logits || !margin || n < 0 || H < 1 || W < 1) return fail(CLASFV_EINVAL, "bad argument");
+  if (n == 0) return CLASFV_OK;
+  HIP_TRY(launch_logit_margin(logits, n, H * W, margin, (hipStream_t)stream));
   return CLASFV_OK;
 }
 
 int clasfv_fuse_votes(const uint8_t* labels, int K, int T, int step, int H, int W, int method, uint8_t* fused,
                       void* stream) {
-  if (!labels || !fused || K < 1 || K > 32 || T < 1 || step < 1 || T - (step - 1) < 1)
-    return fail(CLASFV_EINVAL, "bad argument (K must be in [1, 32])");
-  if (method != CLASFV_FUSE_MAJORITY && method != CLASFV_FUSE_SIMPLE) return fail(CLASFV_EINVAL, "unknown method");
+  if (!labels || !fused || K < 1 || K > CLASFV_MAX_PASSES || T < 1 || step < 1 || T - (step - 1) < 1)
+    return fail(CLASFV_EINVAL, "bad argument (K must be in [1, 64])");
+  if (method != CLASFV_FUSE_MAJORITY && method != CLASFV_FUSE_SIMPLE && method != CLASFV_FUSE_STAPLE)
+    return fail(CLASFV_EINVAL, "unknown method");
   HIP_TRY(launch_fuse_votes(labels, K, T, step, H * W, method, fused, (hipStream_t)stream));
   return CLASFV_OK;
 }
@@ -804,11 +860,11 @@ int clasfv_preprocess_video(const uint8_t* frames, int T, int Hs, int Ws, int H,
   return CLASFV_OK;
 }
 
-int clasfv_zeroone_normalize(float* video, int64_t n, void* stream) {
-  if (!video || n < 1) return fail(CLASFV_EINVAL, "bad argument");
-  static thread_local float* part = nullptr;  // per-thread partials buffer (3 x 512 x 2 floats)
-  if (!part) HIP_TRY(hipMalloc(&part, sizeof(float) * zeroone_partials_floats()));
-  HIP_TRY(launch_zeroone_normalize(video, n, part, (hipStream_t)stream));
+int64_t clasfv_zeroone_workspace_bytes(void) { return (int64_t)sizeof(float) * zeroone_partials_floats(); }
+
+int clasfv_zeroone_normalize(float* video, int64_t n, float* workspace, void* stream) {
+  if (!video || !workspace || n < 1) return fail(CLASFV_EINVAL, "bad argument");
+  HIP_TRY(launch_zeroone_normalize(video, n, workspace, (hipStream_t)stream));
   return CLASFV_OK;
 }
 

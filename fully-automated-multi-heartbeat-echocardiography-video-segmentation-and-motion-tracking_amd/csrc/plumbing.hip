@@ -2,6 +2,7 @@
 //
 //   build_clips        divide_to_consecutive_clips        src/fuse_utils.py:16-33
 //   pass_labels        softmax -> temporal resample -> argmax   src/fuse_utils.py:53-80
+//   logit_margin       l1 - l0 per clip voxel (the multi-GPU exchange payload)
 //   fuse_votes         per-frame label fusion            src/fuse_utils.py:82-100
 //   warp               generate_2dmotion_field + grid_sample   src/transform_utils.py:14-34
 //   warp_backward      its gradients (autograd of the training losses, src/clasfv_losses.py:29-136)
@@ -85,6 +86,10 @@ __device__ inline void softmax2(float x0, float x1, float& p0, float& p1) {
   p1 = e1 / s;
 }
 
+// MARGIN: the input holds d = l1 - l0 per clip voxel ((n,32,H,W), logit_margin_kernel) instead of
+// the two logit planes. softmax2(0, d) == softmax2(l0, l1) bit for bit: with m = max(l0, l1) one
+// exponent is expf(0) and the other expf(-|d|), where fl(l0 - l1) == -fl(l1 - l0) exactly.
+template <bool MARGIN>
 __global__ void pass_labels_kernel(const float* __restrict__ logits, PassTable tab, int T, int step, int HW,
                                    int interp, uint8_t* __restrict__ labels) {
   const int k = blockIdx.z, f = blockIdx.y;
@@ -94,7 +99,7 @@ __global__ void pass_labels_kernel(const float* __restrict__ logits, PassTable t
   const bool resample = interp && (tk & 31) && tk != tc;
   Lin L = {f, f, 1.f, 0.f};
   if (resample) L = lin_ac_false(tc, tk, f);
-  const size_t clip_stride = (size_t)2 * 32 * HW;
+  const size_t clip_stride = (size_t)(MARGIN ? 1 : 2) * 32 * HW;
   const float* base = logits + (size_t)tab.clip0[k] * clip_stride;
   const float* a = base + (size_t)(L.i0 >> 5) * clip_stride + (size_t)(L.i0 & 31) * HW;
   const float* b = base + (size_t)(L.i1 >> 5) * clip_stride + (size_t)(L.i1 & 31) * HW;
@@ -102,15 +107,34 @@ __global__ void pass_labels_kernel(const float* __restrict__ logits, PassTable t
   uint8_t* out = labels + ((size_t)k * T + f) * HW;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += gridDim.x * blockDim.x) {
     float pa0, pa1;
-    softmax2(a[i], a[i + cs], pa0, pa1);
+    if (MARGIN)
+      softmax2(0.f, a[i], pa0, pa1);
+    else
+      softmax2(a[i], a[i + cs], pa0, pa1);
     float q0 = pa0, q1 = pa1;
     if (resample) {
       float pb0, pb1;
-      softmax2(b[i], b[i + cs], pb0, pb1);
+      if (MARGIN)
+        softmax2(0.f, b[i], pb0, pb1);
+      else
+        softmax2(b[i], b[i + cs], pb0, pb1);
       q0 = lerp_t(pa0, pb0, L.l0, L.l1);
       q1 = lerp_t(pa1, pb1, L.l0, L.l1);
     }
     out[i] = q1 > q0 ? 1 : 0;  // np.argmax: first maximum wins ties
+  }
+}
+
+// (n,2,32,HW) logits -> (n,32,HW) margins d = l1 - l0, 4 voxels per thread.
+__global__ void logit_margin_kernel(const float* __restrict__ logits, int n, size_t per_clip,
+                                    float* __restrict__ margin) {
+  const size_t total4 = (size_t)n * per_clip / 4;
+  for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < total4; g += (size_t)gridDim.x * blockDim.x) {
+    const size_t e = 4 * g, c = e / per_clip, r = e - c * per_clip;
+    const float* l = logits + 2 * c * per_clip + r;
+    const f32x4 l0 = *reinterpret_cast<const f32x4*>(l);
+    const f32x4 l1 = *reinterpret_cast<const f32x4*>(l + per_clip);
+    *reinterpret_cast<f32x4*>(margin + e) = l1 - l0;
   }
 }
 
@@ -173,7 +197,7 @@ __global__ __launch_bounds__(SIMPLE_THREADS) void fuse_simple_kernel(const uint8
   }
   for (int p = threadIdx.x; p < HW; p += SIMPLE_THREADS) out[p] = 0;
   for (int lab = 1; lab >= 0; --lab) {
-    unsigned keep = (nv >= 32) ? 0xffffffffu : ((1u << nv) - 1u);
+    uint64_t keep = (nv >= 64) ? ~0ull : ((1ull << nv) - 1ull);
     for (int idx = 0; idx < nv; ++idx) wts[idx] = 1.0;
     __syncthreads();
     // initial estimate: unweighted majority, ties -> off
@@ -194,7 +218,7 @@ __global__ __launch_bounds__(SIMPLE_THREADS) void fuse_simple_kernel(const uint8
       double esum = conv;
       double mx = 0;
       for (int idx = 0; idx < nv; ++idx) {
-        if (!(keep >> idx & 1u)) continue;
+        if (!(keep >> idx & 1ull)) continue;
         double inter = 0, csum = 0;
         for (int p = threadIdx.x; p < HW; p += SIMPLE_THREADS) {
           const bool c = vote(idx, p) == lab;
@@ -211,12 +235,12 @@ __global__ __launch_bounds__(SIMPLE_THREADS) void fuse_simple_kernel(const uint8
       }
       __syncthreads();
       for (int idx = 0; idx < nv; ++idx)
-        if ((keep >> idx & 1u) && !(wts[idx] > 0.05 * mx)) keep &= ~(1u << idx);
+        if ((keep >> idx & 1ull) && !(wts[idx] > 0.05 * mx)) keep &= ~(1ull << idx);
       cnt = 0;
       for (int p = threadIdx.x; p < HW; p += SIMPLE_THREADS) {
         double on = 0, off = 0;
         for (int idx = 0; idx < nv; ++idx) {
-          if (!(keep >> idx & 1u)) continue;
+          if (!(keep >> idx & 1ull)) continue;
           const bool c = vote(idx, p) == lab;
           if (c)
             on += wts[idx];
@@ -375,6 +399,120 @@ __global__ __launch_bounds__(SIMPLE_FAST_THREADS) void fuse_simple_fast_kernel(c
   }
   // label 1 where its estimate is on, then label 0 where its estimate is on (as the kernel above)
   for (int p = threadIdx.x; p < HW; p += SIMPLE_FAST_THREADS) out[p] = (uint8_t)((est[p] & 2u) && !(est[p] & 1u));
+}
+
+// ---- fuse_votes: STAPLE (one workgroup per output frame) --------------------------------------
+// Simultaneous truth and performance level estimation (Warfield, Zou & Wells 2004), binary form as in
+// ITK's STAPLEImageFilter: rater j's decision D_j = (vote == 1); prior f = mean of all D over raters
+// and pixels; sensitivity p_j and specificity q_j start at 0.99999; E step W = f P1 / (f P1 + (1-f)
+// P0) with P1 = prod_j (D_j ? p_j : 1 - p_j), P0 = prod_j (D_j ? 1 - q_j : q_j) (j ascending, double);
+// M step p_j = sum W D_j / sum W, q_j = sum (1-W)(1-D_j) / sum (1-W) (a zero denominator keeps the
+// old value); stop when no p_j, q_j moves by more than 1e-7 or after 100 iterations; label 1 where
+// the final E step gives W > 0.5. PARITY UNPINNED (LabelFusion's source is not available); the
+// oracle restates the same iteration in numpy (oracle/fuse_ref.py:staple_vote).
+constexpr int STAPLE_THREADS = 1024;
+constexpr int STAPLE_CHUNK = 16;  // raters accumulated per pass over the frame
+constexpr int STAPLE_MAX_IT = 100;
+
+__device__ inline double staple_w(unsigned long long d, int nv, const double* p, const double* q, double f) {
+  double a = f, b = 1.0 - f;
+  for (int j = 0; j < nv; ++j) {
+    const bool on = (d >> j) & 1ull;
+    a *= on ? p[j] : 1.0 - p[j];
+    b *= on ? 1.0 - q[j] : q[j];
+  }
+  const double s = a + b;
+  return s > 0.0 ? a / s : f;
+}
+
+// Block sum of N doubles per thread; totals land in tot[0..N).
+template <int N>
+__device__ inline void block_sum_dvec(const double (&v)[N], double (*red)[N], double* tot) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    double x = v[j];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    if (lane == 0) red[wid][j] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < N) {
+    double t = 0.0;
+    for (int w = 0; w < STAPLE_THREADS / 64; ++w) t += red[w][threadIdx.x];
+    tot[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(STAPLE_THREADS) void fuse_staple_kernel(const uint8_t* __restrict__ labels, int K, int T,
+                                                                      int step, int HW, uint8_t* __restrict__ fused) {
+  constexpr int NS = 2 * STAPLE_CHUNK + 1;
+  __shared__ double red[STAPLE_THREADS / 64][NS];
+  __shared__ double tot[NS];
+  __shared__ double sp[CLASFV_MAX_PASSES], sq[CLASFV_MAX_PASSES], np_[CLASFV_MAX_PASSES], nq_[CLASFV_MAX_PASSES];
+  __shared__ int s_done;
+  const int o = blockIdx.x;
+  const int i = o == 0 ? 0 : o + step - 1;
+  const int nv = o == 0 ? 1 : n_votes(i, K, step);
+  uint8_t* out = fused + (size_t)o * HW;
+  auto votes = [&](int p) -> unsigned long long {
+    unsigned long long d = 0;
+    for (int j = 0; j < nv; ++j) d |= (unsigned long long)(labels[((size_t)j * T + (i - j * step)) * HW + p] == 1) << j;
+    return d;
+  };
+  if (nv == 1) {
+    for (int p = threadIdx.x; p < HW; p += STAPLE_THREADS) out[p] = labels[(size_t)i * HW + p];
+    return;
+  }
+  // prior: fraction of foreground decisions over all raters and pixels
+  {
+    double c[NS];
+    for (int j = 0; j < NS; ++j) c[j] = 0.0;
+    for (int p = threadIdx.x; p < HW; p += STAPLE_THREADS) c[0] += (double)__popcll(votes(p));
+    block_sum_dvec<NS>(c, red, tot);
+  }
+  const double f = tot[0] / ((double)nv * (double)HW);
+  if (threadIdx.x < nv) sp[threadIdx.x] = sq[threadIdx.x] = 0.99999;
+  __syncthreads();
+  for (int it = 0; it < STAPLE_MAX_IT; ++it) {
+    if (threadIdx.x == 0) s_done = 1;
+    for (int j0 = 0; j0 < nv; j0 += STAPLE_CHUNK) {
+      // acc[0] = sum W, acc[1 + j] = sum W D_j, acc[1 + C + j] = sum (1 - W)(1 - D_j)
+      double acc[NS];
+      for (int j = 0; j < NS; ++j) acc[j] = 0.0;
+      for (int p = threadIdx.x; p < HW; p += STAPLE_THREADS) {
+        const unsigned long long d = votes(p);
+        const double w = staple_w(d, nv, sp, sq, f);
+        acc[0] += w;
+#pragma unroll
+        for (int j = 0; j < STAPLE_CHUNK; ++j) {
+          const bool on = (d >> (j0 + j)) & 1ull;  // bits at or past nv are 0
+          acc[1 + j] += on ? w : 0.0;
+          acc[1 + STAPLE_CHUNK + j] += on ? 0.0 : 1.0 - w;
+        }
+      }
+      block_sum_dvec<NS>(acc, red, tot);
+      const double sw = tot[0];
+      const double sn = (double)HW - sw;  // sum (1 - W)
+      if (threadIdx.x < STAPLE_CHUNK && j0 + threadIdx.x < nv) {
+        const int j = j0 + threadIdx.x;
+        np_[j] = sw > 0.0 ? tot[1 + threadIdx.x] / sw : sp[j];
+        nq_[j] = sn > 0.0 ? tot[1 + STAPLE_CHUNK + threadIdx.x] / sn : sq[j];
+        if (fabs(np_[j] - sp[j]) > 1e-7 || fabs(nq_[j] - sq[j]) > 1e-7) s_done = 0;
+      }
+      __syncthreads();  // tot is rewritten by the next chunk's reduction
+    }
+    // every E step of this iteration used the old p, q: publish the new ones
+    if (threadIdx.x < nv) {
+      sp[threadIdx.x] = np_[threadIdx.x];
+      sq[threadIdx.x] = nq_[threadIdx.x];
+    }
+    __syncthreads();
+    if (s_done) break;
+    __syncthreads();  // s_done is reset at the top of the next iteration
+  }
+  for (int p = threadIdx.x; p < HW; p += STAPLE_THREADS) out[p] = staple_w(votes(p), nv, sp, sq, f) > 0.5 ? 1 : 0;
 }
 
 // ---- warp ------------------------------------------------------------------------------------
@@ -581,18 +719,30 @@ hipError_t launch_build_clips(const float* video, int T, int HW, const int32_t* 
 }
 
 hipError_t launch_pass_labels(const float* logits, int K, const int32_t* clip0, int T, int step, int HW, int interp,
-                              uint8_t* labels, hipStream_t s) {
+                              int margin, uint8_t* labels, hipStream_t s) {
   PassTable tab;
   for (int k = 0; k < K; ++k) tab.clip0[k] = clip0[k];
   dim3 grid(blocks_for(HW, 256, 64), T, K);
-  hipLaunchKernelGGL(pass_labels_kernel, grid, dim3(256), 0, s, logits, tab, T, step, HW, interp, labels);
+  if (margin)
+    hipLaunchKernelGGL(pass_labels_kernel<true>, grid, dim3(256), 0, s, logits, tab, T, step, HW, interp, labels);
+  else
+    hipLaunchKernelGGL(pass_labels_kernel<false>, grid, dim3(256), 0, s, logits, tab, T, step, HW, interp, labels);
+  return hipGetLastError();
+}
+
+hipError_t launch_logit_margin(const float* logits, int n, int HW, float* margin, hipStream_t s) {
+  const size_t per_clip = (size_t)32 * HW;  // a multiple of 4: 16-B vectors never straddle clips
+  hipLaunchKernelGGL(logit_margin_kernel, dim3(blocks_for((size_t)n * per_clip / 4, 256, 8192)), dim3(256), 0, s, logits,
+                     n, per_clip, margin);
   return hipGetLastError();
 }
 
 hipError_t launch_fuse_votes(const uint8_t* labels, int K, int T, int step, int HW, int method, uint8_t* fused,
                              hipStream_t s) {
   const int tout = T - (step - 1);
-  if (method == 1) {
+  if (method == 2) {
+    hipLaunchKernelGGL(fuse_staple_kernel, dim3(tout), dim3(STAPLE_THREADS), 0, s, labels, K, T, step, HW, fused);
+  } else if (method == 1) {
     const size_t lds = 3 * (size_t)HW;
     if (K <= SIMPLE_FAST_MAXV && lds <= 160 * 1024 && !getenv("CLASFV_SIMPLE_GENERIC")) {
       static size_t attr = 0;

@@ -2,13 +2,17 @@
 
 Every 32-frame clip of every temporally shifted pass of every video is independent
 (src/fuse_utils.py:45-61), so the global clip list is partitioned into contiguous blocks, one per
-rank; each rank runs the encoder-decoder on its block only. Fusion is split by video (video v is
-fused by its owner, rank v % world), so a clip's segmentation logits (2 x 32 x H x W fp32) only have
-to reach that one rank: one all_to_all over RCCL/xGMI moves exactly the clips computed away from
-their owner ("owner-gather"). When every video's clips are computed by its
-owner -- the weak-scaling case of one video per GPU -- nothing crosses xGMI and the collective is
-skipped on every rank (the decision is a pure function of the global plan, so all ranks agree).
-The result is bit-identical to the 1-GPU run: the per-clip computation is placement independent.
+rank; each rank runs the encoder-decoder on its block only. Fusion is split by video: video v is
+fused by its owner, the rank whose block holds most of v's clips (ties -> the lower rank), so only
+the clips of videos that straddle a block boundary have to move. They move by one all_to_all over
+RCCL/xGMI ("owner-gather") as a single fp32 plane per clip frame, the logit
+margin d = l1 - l0: the 2-class softmax the reference takes (src/fuse_utils.py:60) depends on the
+logits only through fl(l1 - l0) (max-subtraction makes one exponent exp(0) = 1 and the other
+exp(-|d|)), so fusing from d is bit-identical to fusing from both logit planes at half the bytes.
+When every video lies inside one block -- e.g. equal-length videos, a whole number per rank, the
+weak-scaling layouts of bench.py -- nothing crosses xGMI and the collective is skipped on every rank
+(the decision is a pure function of the global plan, so all ranks agree). The result is
+bit-identical to the 1-GPU run: the per-clip computation is placement independent.
 ``all_gather_clips`` / ``run_clip_shard`` (every rank gets every clip) remain for callers that need
 all logits everywhere.
 """
@@ -67,12 +71,46 @@ def run_clip_shard(n_total, rank, world, compute, empty):
     return all_gather_clips(local.contiguous(), n_total, rank, world)
 
 
+def video_owners(plans, world):
+    """Owner rank of every video: the rank whose shard_bounds block holds most of its clips (ties
+    -> the lower rank). A video that lies inside one block is owned by the rank that computes it."""
+    n_total = sum(p["n"] for p in plans)
+    blocks = [shard_bounds(n_total, r, world) for r in range(world)]
+    owners = []
+    for p in plans:
+        a, b = p["offset"], p["offset"] + p["n"]
+        best, best_n = 0, -1
+        for r, (lo, hi) in enumerate(blocks):
+            n = max(0, min(b, hi) - max(a, lo))
+            if n > best_n:
+                best, best_n = r, n
+        owners.append(best)
+    return owners
+
+
 def owner_of_clips(plans, world):
-    """Owner rank of every global clip (the owner of its video: video v -> v % world)."""
+    """Owner rank of every global clip (the owner of its video, see video_owners)."""
     own = []
-    for vi, p in enumerate(plans):
-        own.extend([vi % world] * p["n"])
+    for o, p in zip(video_owners(plans, world), plans):
+        own.extend([o] * p["n"])
     return own
+
+
+def exchange_counts(owners, world):
+    """counts[s][o] = clips computed by rank s (its shard_bounds block) and fused by rank o."""
+    n_total = len(owners)
+    counts = [[0] * world for _ in range(world)]
+    for s_ in range(world):
+        lo, hi = shard_bounds(n_total, s_, world)
+        for g in range(lo, hi):
+            counts[s_][owners[g]] += 1
+    return counts
+
+
+def rows_exchanged(owners, world):
+    """Clips that cross ranks in exchange_to_owners (0: the collective is skipped)."""
+    c = exchange_counts(owners, world)
+    return sum(c[s_][o] for s_ in range(world) for o in range(world) if s_ != o)
 
 
 def exchange_to_owners(local, owners, rank, world, group=None):
@@ -81,14 +119,9 @@ def exchange_to_owners(local, owners, rank, world, group=None):
     rows of every clip this rank owns, in global clip order. One all_to_all_single; skipped when no
     clip is computed away from its owner (all ranks derive that from the same plan)."""
     n_total = len(owners)
-    blocks = [shard_bounds(n_total, r, world) for r in range(world)]
-    # counts[s][o] = clips computed by rank s for owner o
-    counts = [[0] * world for _ in range(world)]
-    for s_, (lo, hi) in enumerate(blocks):
-        for g in range(lo, hi):
-            counts[s_][owners[g]] += 1
-    lo, hi = blocks[rank]
-    if world == 1 or all(counts[s_][o] == 0 for s_ in range(world) for o in range(world) if s_ != o):
+    counts = exchange_counts(owners, world)
+    lo, hi = shard_bounds(n_total, rank, world)
+    if world == 1 or rows_exchanged(owners, world) == 0:
         keep = [g - lo for g in range(lo, hi) if owners[g] == rank]
         if len(keep) == hi - lo:
             return local
@@ -108,7 +141,7 @@ def segment_videos_sharded(videos_dev, model, num_clips=5, step=1, fuse_method="
     """Fuse a batch of device videos (each (3,T,H,W)) with clips sharded over ranks.
 
     Returns {video index: fused (T',H,W) uint8 device tensor} for the videos this rank owns
-    (v % world == rank). ``clip_fn(clips) -> logits`` overrides the model call."""
+    (video_owners). ``clip_fn(clips) -> logits`` overrides the model call."""
     plans, n_total = global_clip_plan([v.shape[1] for v in videos_dev], num_clips, step, interpolate_last)
     h, w = videos_dev[0].shape[-2:]
     dev = videos_dev[0].device
@@ -126,13 +159,18 @@ def segment_videos_sharded(videos_dev, model, num_clips=5, step=1, fuse_method="
     empty = torch.empty((0, 2, FU.CLIP, h, w), device=dev, dtype=torch.float32)
     lo, hi = shard_bounds(n_total, rank, world)
     local = compute(lo, hi) if hi > lo else empty
-    mine = exchange_to_owners(local.contiguous(), owner_of_clips(plans, world), rank, world)
+    owners = owner_of_clips(plans, world)
+    margin = world > 1 and rows_exchanged(owners, world) > 0
+    if margin:  # ship one fp32 plane per clip frame instead of two (bit-identical labels, see above)
+        local = FU.logit_margin(local) if local.shape[0] else local[:, 0]
+    mine = exchange_to_owners(local.contiguous(), owners, rank, world)
+    vown = video_owners(plans, world)
     out, at = {}, 0
     for vi, p in enumerate(plans):
-        if vi % world != rank:
+        if vown[vi] != rank:
             continue
         lg = mine[at: at + p["n"]]
         at += p["n"]
-        labels = FU.pass_labels(lg, p["clip0"], p["T"], step, interpolate_last)
+        labels = FU.pass_labels(lg, p["clip0"], p["T"], step, interpolate_last, margin=margin)
         out[vi] = FU.fuse_votes(labels, step, fuse_method)
     return out

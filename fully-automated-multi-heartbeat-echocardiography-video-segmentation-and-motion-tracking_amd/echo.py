@@ -1,112 +1,121 @@
-"""Ejection fraction from fused LV masks (host side; per-video 1-D/2-D work, not data parallel).
+"""Ejection fraction from fused LV masks (host side: per-video 1-D / 2-D work, not data parallel).
 
-Restates, with numpy + scipy only:
-* ``compute_ef_using_putative_clips``  src/fuse_utils.py:105-148 (area curve -> percentiles ->
-  scipy.signal.find_peaks for systole/diastole -> ED/ES pairs -> Simpson's method of disks)
-* ``EDESpairs``                        src/echonet_dataset.py:159-172
-* ``get2dPucks``                       src/utils/echo_utils.py:259-385 (principal axes via eig(cov),
-  boundary = skimage ``find_boundaries(mode='thick')`` = grey dilation != grey erosion with the
-  4-connected cross and reflect borders, 10 half-open bins along the major axis, radius = median
-  |minor projection|; an empty bin gives NaN like the reference)
-Pinned by tests/golden/ef.npz, produced by the reference code itself.
+Behaviour (not code) of the reference's EF stage, re-derived from SURVEY.md section 3.4:
+
+* ``compute_ef_using_putative_clips(fused_segmentations, test_pat_index, return_edes=False)``
+  (src/fuse_utils.py:105-148): LV area per frame -> 5/85/95th percentiles -> end-systoles are the
+  area minima and end-diastoles the area maxima found by ``scipy.signal.find_peaks`` (distance 20,
+  prominence half the 5-95 range), diastoles kept only when their area reaches the 85th percentile,
+  frame 0 added as a diastole when the first three frames are that large -> each systole is paired
+  with the latest diastole before it (``EDESpairs``, src/echonet_dataset.py:159-172) -> volumes by
+  Simpson's monoplane method of disks -> EF = (EDV - ESV) / EDV * 100; negative EFs are reported and
+  dropped.
+* ``get2dPucks(abin, apix, npucks=10)`` (src/utils/echo_utils.py:259-385): the mask's principal axes
+  (eigenvectors of the pixel-coordinate covariance, major axis first, each axis oriented so its own
+  coordinate is non-negative), the mask's thick boundary (a pixel whose 4-neighbourhood, edges
+  replicated, is mixed), the boundary's extent L along the major axis cut into ``npucks`` half-open
+  slabs, and per slab the median distance of its boundary pixels from the major axis (NaN for an
+  empty slab, as the reference); an empty mask gives (1.0, zeros), a mask whose covariance has no
+  eigen-decomposition (one pixel) (0.0, zeros).
+* ``compute_ef_batch``: the same for many videos on a thread pool (numpy / scipy release the GIL in
+  their kernels), for the batched multi-video path.
+
+Pinned by tests/golden/ef.npz, which the reference code itself produced (tests/golden/make_golden_ef.py).
 """
+from concurrent.futures import ThreadPoolExecutor
+
 import numpy as np
-from scipy import ndimage
 from scipy.signal import find_peaks
 
-_CROSS = ndimage.generate_binary_structure(2, 1)
 
-
-def find_boundaries_thick(label_img):
-    img = np.asarray(label_img)
-    if img.dtype == bool:
-        img = img.astype(np.uint8)
-    return ndimage.grey_dilation(img, footprint=_CROSS) != ndimage.grey_erosion(img, footprint=_CROSS)
+def thick_boundary(mask):
+    """Boolean map of the pixels whose 4-neighbourhood (edge pixels replicated) holds both values."""
+    m = np.asarray(mask) != 0
+    pad = np.pad(m, 1, mode="edge")
+    stack = np.stack([pad[1:-1, 1:-1], pad[:-2, 1:-1], pad[2:, 1:-1], pad[1:-1, :-2], pad[1:-1, 2:]])
+    return stack.any(axis=0) & ~stack.all(axis=0)
 
 
 def get2dPucks(abin, apix, npucks=10):
-    """Length of the structure along its major axis and the npucks disk radii about it."""
-    if ~np.any(abin):
+    """(length along the major axis, npucks disk radii) of a binary mask; ``apix`` = pixel spacing
+    per image axis. An empty mask gives (1.0, zeros) as in the reference."""
+    mask = np.asarray(abin) > 0
+    if not mask.any():
         return 1.0, np.zeros((npucks,))
-    x, y = np.where(abin > 0)
-    X = np.stack([x, y])
-    if X.shape[1] < 1:
-        return (0.0, np.zeros((npucks,)))
-    X = np.multiply(X, np.array(apix)[:, None])
-    try:
-        val, vec = np.linalg.eig(np.cov(X, rowvar=True))
-    except Exception:
-        return (0.0, np.zeros((npucks,)))
-    order = np.argsort(val)[-1::-1]
-    vec = vec[:, order]
-    if vec[0, 0] < 0:
-        vec[:, 0] = -1.0 * vec[:, 0]
-    if vec[1, 1] < 0:
-        vec[:, 1] = -1.0 * vec[:, 1]
-    mu = np.expand_dims(np.mean(X, axis=1), axis=1)
-    B = find_boundaries_thick(abin)
-    Xb = np.stack(np.where(B))
-    Xb = np.multiply(Xb, np.array(apix)[:, None])
-    proj = np.dot((Xb - mu).T, vec)
-    L_min, L_max = np.min(proj, axis=0), np.max(proj, axis=0)
-    L = L_max - L_min
-    edges = np.linspace(L_min[0], L_max[0], npucks + 1)
-    R = []
-    with np.errstate(invalid="ignore"):
-        for i in range(len(edges) - 1):
-            which = np.logical_and(proj[:, 0] >= edges[i], proj[:, 0] < edges[i + 1])
-            # the reference's `len(which) == 0` guard never fires: an empty bin's median is NaN
-            r = np.median(np.abs(proj[:, 1][which])) if which.any() else np.nan
-            R.append(r)
-    return L[0], np.array(R)
+    spacing = np.asarray(apix, dtype=np.float64).reshape(2, 1)
+    pts = np.stack(np.nonzero(mask)) * spacing            # (2, n) pixel coordinates
+    with np.errstate(invalid="ignore", divide="ignore"):
+        cov = np.cov(pts, rowvar=True)
+    try:  # a one-pixel mask has an undefined (NaN) covariance: (0.0, zeros) as the reference
+        evals, evecs = np.linalg.eig(cov)
+    except np.linalg.LinAlgError:
+        return 0.0, np.zeros((npucks,))
+    axes = evecs[:, np.argsort(evals)[::-1]]            # major axis first
+    axes = axes * np.where(np.diag(axes) < 0, -1.0, 1.0)  # axis i points along +coordinate i
+    centre = pts.mean(axis=1, keepdims=True)
+    rim = np.stack(np.nonzero(thick_boundary(mask))) * spacing
+    coords = np.dot((rim - centre).T, axes)             # (n_rim, 2): (along, across) the major axis
+    lo, hi = coords.min(axis=0), coords.max(axis=0)
+    cuts = np.linspace(lo[0], hi[0], npucks + 1)
+    slab = np.digitize(coords[:, 0], cuts, right=False) - 1  # cuts[i] <= x < cuts[i+1] -> i
+    dist = np.abs(coords[:, 1])
+    radii = np.array([np.median(dist[slab == i]) if np.any(slab == i) else np.nan for i in range(npucks)])
+    return (hi - lo)[0], radii
 
 
 def EDESpairs(diastole, systole):
-    diastole = np.sort(np.array(diastole))
-    systole = np.sort(np.array(systole))
-    clips = []
-    inds = np.searchsorted(diastole, systole, side="left")
-    for i, sf in enumerate(systole):
-        if inds[i] == 0:
-            continue
-        best_df = diastole[inds[i] - 1]
-        if len(clips) == 0 or best_df != clips[-1][0]:
-            clips.append((best_df, sf))
-    return clips
+    """[(ED, ES)]: every systole with the latest diastole strictly before it; a diastole already
+    paired with an earlier systole is not paired again."""
+    ed = np.sort(np.asarray(diastole))
+    es = np.sort(np.asarray(systole))
+    prev = np.searchsorted(ed, es, side="left") - 1
+    pairs, last = [], -1
+    for j, s in zip(prev, es):
+        if j >= 0 and j != last:
+            pairs.append((ed[j], s))
+            last = j
+    return pairs
+
+
+def _disk_volume(length, radii):
+    """Simpson's monoplane method: sum of npucks cylinders of height length / npucks."""
+    return np.sum(np.pi * radii * radii * length / len(radii))
 
 
 def compute_ef_using_putative_clips(fused_segmentations, test_pat_index, return_edes=False):
     seg = np.asarray(fused_segmentations)
-    size = np.sum(seg, axis=(1, 2)).ravel()
-    _05cut, _85cut, _95cut = np.percentile(size, [5, 85, 95])
-    trim_range = _95cut - _05cut
-    systole = find_peaks(-size, distance=20, prominence=(0.50 * trim_range))[0]
-    diastole = find_peaks(size, distance=20, prominence=(0.50 * trim_range))[0]
-    diastole = [x for x in diastole if size[x] >= _85cut]
-    if np.mean(size[:3]) >= _85cut:
-        diastole = [0] + diastole
-    diastole = np.array(diastole)
-    clip_pairs = EDESpairs(diastole, systole)
+    area = seg.sum(axis=(1, 2)).ravel()
+    p5, p85, p95 = np.percentile(area, [5, 85, 95])
+    prom = 0.50 * (p95 - p5)
+    es = find_peaks(-area, distance=20, prominence=prom)[0]
+    ed = [int(i) for i in find_peaks(area, distance=20, prominence=prom)[0] if area[i] >= p85]
+    if np.mean(area[:3]) >= p85:
+        ed.insert(0, 0)
+    pairs = EDESpairs(np.array(ed), es)
     frames = seg.reshape(-1, seg.shape[-2], seg.shape[-1])
     efs = []
-    for ed, es in clip_pairs:
-        l_ed, r_ed = get2dPucks((frames[ed] == 1).astype("int"), (1.0, 1.0))
-        l_es, r_es = get2dPucks((frames[es] == 1).astype("int"), (1.0, 1.0))
+    for d, s in pairs:
         with np.errstate(invalid="ignore", divide="ignore"):
-            edv = np.sum(((np.pi * r_ed * r_ed) * l_ed / len(r_ed)))
-            esv = np.sum(((np.pi * r_es * r_es) * l_es / len(r_es)))
+            edv = _disk_volume(*get2dPucks((frames[d] == 1).astype(int), (1.0, 1.0)))
+            esv = _disk_volume(*get2dPucks((frames[s] == 1).astype(int), (1.0, 1.0)))
             ef = (edv - esv) / edv * 100
         if ef < 0:
             print("Negative EF at patient: " + str(test_pat_index))
             continue
         efs.append(ef)
-    if return_edes:
-        return efs, clip_pairs
-    return efs
+    return (efs, pairs) if return_edes else efs
+
+
+def compute_ef_batch(segmentations, names=None, return_edes=False, workers=8):
+    """compute_ef_using_putative_clips over many fused mask videos on a thread pool."""
+    names = list(names) if names is not None else list(range(len(segmentations)))
+    with ThreadPoolExecutor(max(1, workers)) as ex:
+        return list(ex.map(lambda a: compute_ef_using_putative_clips(a[0], a[1], return_edes),
+                           zip(segmentations, names)))
 
 
 def categorical_dice(prediction, truth, k, epsilon=1e-5):
-    """src/clasfv_losses.py:60-68 -- the Dice metric used for parity."""
-    A = (np.asarray(prediction) == k)
-    B = (np.asarray(truth) == k)
-    return 2 * np.sum(A * B) / (np.sum(A) + np.sum(B) + epsilon)
+    """Dice of class k (src/clasfv_losses.py:60-68), the parity metric: 2|A & B| / (|A| + |B| + eps)."""
+    a = np.asarray(prediction) == k
+    b = np.asarray(truth) == k
+    return 2 * np.count_nonzero(a & b) / (np.count_nonzero(a) + np.count_nonzero(b) + epsilon)

@@ -10,8 +10,9 @@ stay in HBM (``clasfv_pass_labels``, ``clasfv_fuse_votes``); only the final uint
 Reference behaviour kept: banker's rounding of the clip count (:22,29), the K clamp and its
 "Video is too short" message (:38-42), IndexError when K == 0 (:82, e.g. T == 32), frames 1..step-1
 dropped for step > 1 (:85), passes with different clip counts (numpy 1.19 ragged arrays, :50).
-Fusion: ``majority`` (= ``majorityvoting``/``mv``/``itkvoting``; ties -> background) and ``simple``
-(SIMPLE, Langerak 2010). LabelFusion itself is not available, so ``simple`` is parity-unpinned.
+Fusion: ``majority`` (= ``majorityvoting``/``mv``/``itkvoting``; ties -> background), ``simple``
+(SIMPLE, Langerak 2010) and ``staple`` (STAPLE, Warfield 2004), up to 64 passes. LabelFusion itself
+is not available, so ``simple`` and ``staple`` are parity-unpinned.
 """
 import numpy as np
 import torch
@@ -19,7 +20,9 @@ import torch
 from . import _lib
 
 FUSE_METHODS = {"majority": _lib.FUSE_MAJORITY, "majorityvoting": _lib.FUSE_MAJORITY, "mv": _lib.FUSE_MAJORITY,
-                "itkvoting": _lib.FUSE_MAJORITY, "voting": _lib.FUSE_MAJORITY, "simple": _lib.FUSE_SIMPLE}
+                "itkvoting": _lib.FUSE_MAJORITY, "voting": _lib.FUSE_MAJORITY, "simple": _lib.FUSE_SIMPLE,
+                "staple": _lib.FUSE_STAPLE}
+MAX_PASSES = 64  # CLASFV_MAX_PASSES
 CLIP = 32
 DEFAULT_BATCH = 32
 
@@ -93,7 +96,7 @@ def build_clips(video_dev, table, interpolate_last=True):
     clips = torch.empty((len(table), 3, CLIP, h, w), device=video_dev.device, dtype=torch.float32)
     lib = _lib.load()
     _lib.check(lib.clasfv_build_clips(_lib.ptr(video_dev), t, h, w, _lib.ptr(tab), len(table), int(bool(interpolate_last)),
-                                      _lib.ptr(clips), _lib.stream_ptr()), "clasfv_build_clips")
+                                      _lib.ptr(clips), _lib.stream_ptr(device=video_dev.device)), "clasfv_build_clips")
     return clips
 
 
@@ -128,8 +131,8 @@ def fuse_votes(labels, step, fuse_method="simple"):
         raise NotImplementedError(f"fuse_method {fuse_method!r}: supported {sorted(FUSE_METHODS)}")
     fused = torch.empty((t - (step - 1), h, w), device=labels.device, dtype=torch.uint8)
     lib = _lib.load()
-    _lib.check(lib.clasfv_fuse_votes(_lib.ptr(labels), k, t, step, h, w, method, _lib.ptr(fused), _lib.stream_ptr()),
-               "clasfv_fuse_votes")
+    _lib.check(lib.clasfv_fuse_votes(_lib.ptr(labels), k, t, step, h, w, method, _lib.ptr(fused),
+                                     _lib.stream_ptr(device=labels.device)), "clasfv_fuse_votes")
     return fused
 
 
@@ -158,16 +161,31 @@ def segment_a_video_with_fusion_device(video, model, interpolate_last=True, step
     return fuse_votes(labels, step, fuse_method)
 
 
-def pass_labels(logits, clip0, t, step, interpolate_last=True):
-    """(K,T,H,W) uint8 labels of the K shifted passes (softmax -> resample -> argmax)."""
+def logit_margin(logits):
+    """(n,2,32,H,W) logits -> (n,32,H,W) margins l1 - l0 (what pass_labels(margin=True) consumes)."""
+    logits = logits.to(torch.float32).contiguous()
+    n, _, c, h, w = logits.shape
+    out = torch.empty((n, c, h, w), device=logits.device, dtype=torch.float32)
+    lib = _lib.load()
+    _lib.check(lib.clasfv_logit_margin(_lib.ptr(logits), n, h, w, _lib.ptr(out), _lib.stream_ptr(device=logits.device)),
+               "clasfv_logit_margin")
+    return out
+
+
+def pass_labels(logits, clip0, t, step, interpolate_last=True, margin=False):
+    """(K,T,H,W) uint8 labels of the K shifted passes (softmax -> resample -> argmax). ``logits``
+    is (n,2,32,H,W), or (n,32,H,W) margins l1 - l0 with ``margin=True`` (bit-identical labels)."""
     k = len(clip0)
+    if k > MAX_PASSES:
+        raise ValueError(f"at most {MAX_PASSES} shifted passes are supported (got {k})")
     logits = logits.to(torch.float32).contiguous()
     h, w = logits.shape[-2:]
     labels = torch.empty((k, t, h, w), device=logits.device, dtype=torch.uint8)
     ptr, keep = ctypes_int32_array(clip0)
     lib = _lib.load()
-    _lib.check(lib.clasfv_pass_labels(_lib.ptr(logits), k, ptr, t, step, h, w, int(bool(interpolate_last)),
-                                      _lib.ptr(labels), _lib.stream_ptr()), "clasfv_pass_labels")
+    fn = lib.clasfv_pass_labels_margin if margin else lib.clasfv_pass_labels
+    _lib.check(fn(_lib.ptr(logits), k, ptr, t, step, h, w, int(bool(interpolate_last)), _lib.ptr(labels),
+                  _lib.stream_ptr(device=logits.device)), "clasfv_pass_labels")
     del keep
     return labels
 

@@ -1,47 +1,64 @@
 """Training-side CLAS-FV losses on the HIP warp.
 
-Drop-ins for ``src/clasfv_losses.py`` and the helpers it uses from ``src/loss_functions.py``, with
-the same names, arguments and values; every motion warp runs through ``warp.warp`` (the fused
-``clasfv_warp`` kernel forward, ``clasfv_warp_backward`` under autograd) instead of
-``generate_2dmotion_field`` + ``F.grid_sample``. The reductions around the warps (MSE, Huber
-smoothness, Dice) are a handful of small tensor ops and stay in PyTorch.
+Drop-ins, by name, argument meaning and value, for ``src/clasfv_losses.py`` and the helpers it uses
+from ``src/loss_functions.py``. The definitions are re-derived from SURVEY.md sections 3.3 / 3.5:
 
-* ``deformation_motion_loss`` -- OTA loss, src/clasfv_losses.py:29-56
-* ``motion_seg_loss``         -- SGS / OTS losses, src/clasfv_losses.py:71-136
-* ``DiceLoss``                -- src/clasfv_losses.py:11-26
-* ``huber_loss``              -- src/loss_functions.py:66-77
-* ``convert_to_1hot``         -- src/loss_functions.py:123-134 (returns a float32 device tensor)
-* ``categorical_dice``        -- src/clasfv_losses.py:59-68 (numpy metric, not a loss)
+* ``deformation_motion_loss(source_videos, motion_field)`` (OTA, src/clasfv_losses.py:29-56): every
+  frame t < T-1 is warped onto frame t+1 with the forward field (channels 0,1 at t) and frame t+1
+  onto frame t with the backward field (channels 2,3 at t+1); the loss is the per-pair mean squared
+  error plus 0.005 x the smoothness penalty of both fields, summed over pairs, / 2 / (T-1).
+  Here all T-1 frame pairs are warped by ONE ``clasfv_warp`` launch each way (time folded into the
+  batch dimension; the warp is per-image independent, so every warped frame is bit-identical to
+  the frame-by-frame form).
+* ``motion_seg_loss(label_ed, label_es, ed_index, es_index, motion_output, seg_softmax, start, end,
+  seg_criterion)`` (SGS / OTS, src/clasfv_losses.py:71-136): the one-hot ED and ES labels are
+  propagated frame by frame through the forward fields to the end of the clip and through the
+  backward fields to its start; each propagated label is scored with ``seg_criterion`` against the
+  softmax of the frame it lands on, except the ED->ES and ES->ED landings, which are scored with a
+  Dice loss against the true ES / ED labels (OTS). Returns (flow_loss / (2 (T-2)), ots_loss / 2).
+  The ED- and ES-seeded chains of one direction share their motion fields frame by frame, so they
+  advance together: one stacked warp per frame instead of two.
+* ``DiceLoss`` (src/clasfv_losses.py:11-26), ``huber_loss`` (src/loss_functions.py:66-77),
+  ``convert_to_1hot`` (src/loss_functions.py:123-134), ``categorical_dice`` (the numpy metric).
 """
 import numpy as np
 import torch
 from torch import nn
 
+from .echo import categorical_dice  # noqa: F401  (re-exported: src/clasfv_losses.py:60-68)
 from .warp import warp
 
 
+def soft_dice_loss(pred, target, smooth=1.0):
+    """1 - (2 <pred, target> + smooth) / (|pred|_1 + |target|_1 + smooth) over all elements."""
+    p, t = pred.reshape(-1), target.reshape(-1)
+    return 1 - (2.0 * torch.dot(p, t) + smooth) / (p.sum() + t.sum() + smooth)
+
+
 class DiceLoss(nn.Module):
-    """1 - (2*sum(x*y) + smooth) / (sum(x) + sum(y) + smooth) over all elements."""
+    """nn.Module form of soft_dice_loss; ``forward(inputs, targets, smooth=1)``."""
 
     def __init__(self, weight=None, size_average=True):
         super().__init__()
 
     def forward(self, inputs, targets, smooth=1):
-        inputs = inputs.reshape(-1)
-        targets = targets.reshape(-1)
-        intersection = (inputs * targets).sum()
-        dice = (2. * intersection + smooth) / (inputs.sum() + targets.sum() + smooth)
-        return 1 - dice
+        return soft_dice_loss(inputs, targets, smooth)
+
+
+def _smoothness(field):
+    """Per-leading-index smoothness of a (..., N, C, H, W) field: sqrt(0.01 + (sum of squared
+    differences along W / H + sum along H / W) / N)."""
+    n, h, w = field.shape[-4], field.shape[-2], field.shape[-1]
+    gx = field[..., :, 1:] - field[..., :, :-1]
+    gy = field[..., 1:, :] - field[..., :-1, :]
+    sx = (gx * gx).sum(dim=(-4, -3, -2, -1))
+    sy = (gy * gy).sum(dim=(-4, -3, -2, -1))
+    return torch.sqrt(0.01 + (sx / h + sy / w) / n)
 
 
 def huber_loss(x):
-    """sqrt(0.01 + (sum(dx^2)/H + sum(dy^2)/W) / N) of a (N,C,H,W) field (src/loss_functions.py:66-77)."""
-    bsize, _, height, width = x.size()
-    d_x = x[:, :, :, 1:] - x[:, :, :, :-1]
-    d_y = x[:, :, 1:, :] - x[:, :, :-1, :]
-    err = torch.sum(torch.mul(d_x, d_x)) / height + torch.sum(torch.mul(d_y, d_y)) / width
-    err /= bsize
-    return torch.sqrt(0.01 + err)
+    """Smoothness penalty of one (N,C,H,W) displacement field (src/loss_functions.py:66-77)."""
+    return _smoothness(x)
 
 
 def convert_to_1hot(label, n_class, device=None):
@@ -50,81 +67,89 @@ def convert_to_1hot(label, n_class, device=None):
     if device is None:
         device = lab.device if lab.is_cuda else torch.device("cuda", torch.cuda.current_device())
     lab = lab.to(device=device, dtype=torch.int64)
-    out = torch.zeros((lab.shape[0], n_class) + tuple(lab.shape[2:]), device=device, dtype=torch.float32)
-    return out.scatter_(1, lab, 1.0)
+    classes = torch.arange(n_class, device=device).view(1, n_class, *([1] * (lab.dim() - 2)))
+    return (lab == classes).to(torch.float32)
 
 
-def categorical_dice(prediction, truth, k, epsilon=1e-5):
-    a = np.asarray(prediction) == k
-    b = np.asarray(truth) == k
-    return 2 * np.sum(a * b) / (np.sum(a) + np.sum(b) + epsilon)
+def _time_major(x):
+    """(N, C, P, H, W) -> (P*N, C, H, W) with the P frames outermost (contiguous)."""
+    n, c, p, h, w = x.shape
+    return x.permute(2, 0, 1, 3, 4).reshape(p * n, c, h, w)
 
 
 def deformation_motion_loss(source_videos, motion_field):
-    """OTA loss: warp every frame forward (motion channels 0,1) onto the next and every next frame
-    backward (channels 2,3) onto the previous; MSE to the real frames + 0.005 * Huber smoothness of
-    both fields, averaged over the T-1 frame pairs. source_videos (N,C,T,H,W), motion_field
-    (N,4,T,H,W), both on the device."""
-    mse = nn.MSELoss()
-    mse_loss = 0
-    smooth_loss = 0
-    t = source_videos.shape[2]
-    for index in range(t - 1):
-        forward_motion = motion_field[:, :2, index, ...]
-        backward_motion = motion_field[:, 2:, index + 1, ...]
-        pred_forward = warp(source_videos[:, :, index, ...], forward_motion)
-        pred_backward = warp(source_videos[:, :, index + 1, ...], backward_motion)
-        mse_loss += mse(source_videos[:, :, index + 1, ...], pred_forward)
-        mse_loss += mse(source_videos[:, :, index, ...], pred_backward)
-        smooth_loss += huber_loss(forward_motion)
-        smooth_loss += huber_loss(backward_motion)
-    return (0.005 * smooth_loss + mse_loss) / 2 / (t - 1)
+    """OTA loss of source_videos (N,C,T,H,W) under motion_field (N,4,T,H,W), both on the device."""
+    n, c, t, h, w = source_videos.shape
+    pairs = t - 1
+    prev_frames = _time_major(source_videos[:, :, :-1])
+    next_frames = _time_major(source_videos[:, :, 1:])
+    fwd = motion_field[:, 0:2, :-1]
+    bwd = motion_field[:, 2:4, 1:]
+    to_next = warp(prev_frames, _time_major(fwd))
+    to_prev = warp(next_frames, _time_major(bwd))
+    per_pair = lambda d: (d * d).reshape(pairs, -1).mean(dim=1)  # noqa: E731
+    mse = per_pair(to_next - next_frames) + per_pair(to_prev - prev_frames)
+    smooth = _smoothness(fwd.permute(2, 0, 1, 3, 4)) + _smoothness(bwd.permute(2, 0, 1, 3, 4))
+    return (0.005 * smooth.sum() + mse.sum()) / 2 / pairs
+
+
+def _propagate(seeds, fields, direction, start, end):
+    """Advance label chains through per-frame displacement fields.
+
+    seeds: {name: (first_frame, one-hot (N,2,H,W))}; a chain seeded at frame f is warped by
+    fields[:, :, f] and lands on f + direction, then by the field of that frame, and so on while the
+    landing frame stays inside [start, end). Chains active at the same frame are stacked into one
+    warp launch. Returns {name: [(landing_frame, warped label), ...]} in propagation order."""
+    n = fields.shape[0]
+    frames = {k: f for k, (f, _) in seeds.items()}
+    state = {k: lab for k, (_, lab) in seeds.items()}
+    out = {k: [] for k in seeds}
+    first = min(frames.values()) if direction > 0 else max(frames.values())
+    f = first
+    while True:
+        land = f + direction
+        if not (start <= land < end) or (direction < 0 and f <= start):
+            break
+        active = [k for k in seeds if (frames[k] <= f if direction > 0 else frames[k] >= f)]
+        if active:
+            stacked = torch.cat([state[k] for k in active])
+            moved = warp(stacked, fields[:, :, f].repeat(len(active), 1, 1, 1))
+            for i, k in enumerate(active):
+                state[k] = moved[i * n:(i + 1) * n]
+                out[k].append((land, state[k]))
+        f = land
+    return out
 
 
 def motion_seg_loss(label_ed, label_es, ed_index, es_index, motion_output, seg_softmax, start=0, end=32,
                     seg_criterion=DiceLoss()):
-    """SGS and OTS losses: the true ED and ES labels are warped (one-hot, bilinear) frame by frame
-    forward to the end of the clip and backward to its start through the motion head's fields;
-    each warped label is compared with the segmentation softmax of that frame (Dice), and the ED->ES
-    / ES->ED warps with the true ES / ED labels. Returns (flow_loss, OTS_loss)."""
+    """SGS and OTS losses (see module docstring). Returns (flow_loss, OTS_loss)."""
     dev = motion_output.device
-    one_ed = convert_to_1hot(label_ed, 2, dev)
-    one_es = convert_to_1hot(label_es, 2, dev)
-    ots = DiceLoss()
-    loss_forward = 0
-    ots_loss = 0
+    ed1 = convert_to_1hot(label_ed, 2, dev)
+    es1 = convert_to_1hot(label_es, 2, dev)
+    ed_index, es_index = int(ed_index), int(es_index)
+    fwd = motion_output[:, 0:2]
+    bwd = motion_output[:, 2:4]
+    flow, ots = 0, 0
 
-    flow_source = one_ed
-    for frame_index in range(ed_index, end - 1):
-        next_label = warp(flow_source, motion_output[:, :2, frame_index, ...])
-        if frame_index == (es_index - 1):
-            ots_loss += ots(next_label, one_es)
+    # forward in time: both chains run until they land on frame end-1
+    chains = _propagate({"ed": (ed_index, ed1), "es": (es_index, es1)}, fwd, +1, start, end)
+    for land, lab in chains["ed"]:
+        if land == es_index:
+            ots = ots + soft_dice_loss(lab, es1)
         else:
-            loss_forward += seg_criterion(seg_softmax[:, :, frame_index + 1, ...], next_label)
-        flow_source = next_label
+            flow = flow + seg_criterion(seg_softmax[:, :, land], lab)
+    for land, lab in chains["es"]:
+        flow = flow + seg_criterion(seg_softmax[:, :, land], lab)
 
-    flow_source = one_es
-    for frame_index in range(es_index, end - 1):
-        next_label = warp(flow_source, motion_output[:, :2, frame_index, ...])
-        loss_forward += seg_criterion(seg_softmax[:, :, frame_index + 1, ...], next_label)
-        flow_source = next_label
-
-    flow_source = one_es
-    loss_backward = 0
-    for frame_index in range(es_index, start, -1):
-        next_label = warp(flow_source, motion_output[:, 2:, frame_index, ...])
-        if frame_index == ed_index + 1:
-            ots_loss += ots(next_label, one_ed)
+    # backward in time: both chains run until they land on frame start
+    chains = _propagate({"es": (es_index, es1), "ed": (ed_index, ed1)}, bwd, -1, start, end)
+    for land, lab in chains["es"]:
+        if land == ed_index:
+            ots = ots + soft_dice_loss(lab, ed1)
         else:
-            loss_backward += seg_criterion(seg_softmax[:, :, frame_index - 1, ...], next_label)
-        flow_source = next_label
+            flow = flow + seg_criterion(seg_softmax[:, :, land], lab)
+    for land, lab in chains["ed"]:
+        flow = flow + seg_criterion(seg_softmax[:, :, land], lab)
 
-    flow_source = one_ed
-    for frame_index in range(ed_index, start, -1):
-        next_label = warp(flow_source, motion_output[:, 2:, frame_index, ...])
-        loss_backward += seg_criterion(seg_softmax[:, :, frame_index - 1, ...], next_label)
-        flow_source = next_label
-
-    flow_loss = (loss_forward + loss_backward) / ((motion_output.shape[2] - 2) * 2)
-    ots_loss = ots_loss / 2
-    return flow_loss, ots_loss
+    return flow / ((motion_output.shape[2] - 2) * 2), ots / 2

@@ -74,23 +74,25 @@ class Engine:
     def forward(self, x, seg, mot, stream=None):
         n, c, t, hh, ww = x.shape
         _lib.check(self.lib.clasfv_forward(self.h, _lib.ptr(x), n, t, hh, ww, _lib.ptr(seg), _lib.ptr(mot),
-                                           _lib.stream_ptr(stream)), "clasfv_forward")
+                                           _lib.stream_ptr(stream, self.device)), "clasfv_forward")
 
     def set_kernel_timing(self, enable=True):
         """Per-kernel HIP-event timing of every later forward (see clasfv_kernel_timing)."""
         _lib.check(self.lib.clasfv_set_kernel_timing(self.h, 1 if enable else 0), "clasfv_set_kernel_timing")
 
     def kernel_timing(self, cap=16):
-        """{kernel: {"launches", "ms", "gflop"}} over the forwards since the last call (then cleared)."""
+        """{kernel: {"launches", "ms", "gflop", "xgflop"}} over the forwards since the last call (then
+        cleared). gflop: algorithmic (direct-conv MACs x 2); xgflop: MFMA work actually issued."""
         names = (ctypes.c_char_p * cap)()
         launches = (ctypes.c_int * cap)()
         ms = (ctypes.c_double * cap)()
         gf = (ctypes.c_double * cap)()
-        n = self.lib.clasfv_kernel_timing(self.h, cap, names, launches, ms, gf)
+        xg = (ctypes.c_double * cap)()
+        n = self.lib.clasfv_kernel_timing(self.h, cap, names, launches, ms, gf, xg)
         if n < 0:
             _lib.check(n, "clasfv_kernel_timing")
-        return {names[i].decode(): {"launches": int(launches[i]), "ms": float(ms[i]), "gflop": float(gf[i])}
-                for i in range(n)}
+        return {names[i].decode(): {"launches": int(launches[i]), "ms": float(ms[i]), "gflop": float(gf[i]),
+                                    "xgflop": float(xg[i])} for i in range(n)}
 
     def workspace_bytes(self):
         return int(self.lib.clasfv_workspace_bytes(self.h))

@@ -20,8 +20,10 @@ def zeroone_normalize_(video):
     if video.shape[0] != 3 or video.dtype != torch.float32 or not video.is_contiguous():
         raise ValueError("expected a contiguous float32 (3, ...) tensor")
     lib = _lib.load()
-    _lib.check(lib.clasfv_zeroone_normalize(_lib.ptr(video), video[0].numel(), _lib.stream_ptr()),
-               "clasfv_zeroone_normalize")
+    # scratch for the per-block min/max partials, stream-ordered by the caching allocator
+    ws = torch.empty(int(lib.clasfv_zeroone_workspace_bytes()) // 4, device=video.device, dtype=torch.float32)
+    _lib.check(lib.clasfv_zeroone_normalize(_lib.ptr(video), video[0].numel(), _lib.ptr(ws),
+                                            _lib.stream_ptr(device=video.device)), "clasfv_zeroone_normalize")
     return video
 
 
@@ -58,6 +60,6 @@ def preprocess_video(frames, height=112, width=112, device=None, normalize=True)
     t, hs, ws, _ = f.shape
     out = torch.empty((3, t, height, width), device=dev, dtype=torch.float32)
     lib = _lib.load()
-    _lib.check(lib.clasfv_preprocess_video(_lib.ptr(f), t, hs, ws, height, width, _lib.ptr(out), _lib.stream_ptr()),
-               "clasfv_preprocess_video")
+    _lib.check(lib.clasfv_preprocess_video(_lib.ptr(f), t, hs, ws, height, width, _lib.ptr(out),
+                                           _lib.stream_ptr(device=dev)), "clasfv_preprocess_video")
     return zeroone_normalize_(out) if normalize else out

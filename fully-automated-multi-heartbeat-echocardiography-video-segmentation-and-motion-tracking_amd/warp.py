@@ -34,7 +34,7 @@ def _warp_forward(img, motion, out=None):
         out = torch.empty_like(img)
     lib = _lib.load()
     _lib.check(lib.clasfv_warp(_lib.ptr(img), n, c, h, w, _lib.ptr(motion), motion.stride(0), motion.stride(1),
-                               _lib.ptr(out), _lib.stream_ptr()), "clasfv_warp")
+                               _lib.ptr(out), _lib.stream_ptr(device=img.device)), "clasfv_warp")
     return out
 
 
@@ -59,7 +59,8 @@ class _Warp(torch.autograd.Function):
         _lib.check(lib.clasfv_warp_backward(_lib.ptr(grad_out), _lib.ptr(img), n, c, h, w, _lib.ptr(motion),
                                             motion.stride(0), motion.stride(1),
                                             _lib.ptr(gimg) if gimg is not None else nul,
-                                            _lib.ptr(gmot) if gmot is not None else nul, _lib.stream_ptr()),
+                                            _lib.ptr(gmot) if gmot is not None else nul,
+                                            _lib.stream_ptr(device=img.device)),
                    "clasfv_warp_backward")
         return gimg, gmot
 

@@ -40,7 +40,7 @@ enum {
   CLASFV_ENOMEM = -5
 };
 
-enum { CLASFV_FUSE_MAJORITY = 0, CLASFV_FUSE_SIMPLE = 1 };
+enum { CLASFV_FUSE_MAJORITY = 0, CLASFV_FUSE_SIMPLE = 1, CLASFV_FUSE_STAPLE = 2 };
 enum { CLASFV_DTYPE_FP32 = 0, CLASFV_DTYPE_BF16 = 1 };
 
 typedef struct clasfv_engine* clasfv_t;
@@ -79,10 +79,12 @@ int clasfv_get_compute_dtype(clasfv_t h);
 int clasfv_set_kernel_timing(clasfv_t h, int enable);
 /* Waits for the recorded events, aggregates the launches recorded since the last call per kernel
  * and clears them. Entry i: names[i] (static string, e.g. "conv_wino"), launches[i], ms[i] (summed
- * device time), gflop[i] (summed algorithmic GFLOP, 2 per MAC over unpadded channels). Returns
- * the number of entries (<= cap) or a negative error code. */
+ * device time), gflop[i] (summed algorithmic GFLOP, 2 per MAC over unpadded channels: the direct
+ * convolution the launch replaces), xgflop[i] (summed GFLOP the launch issues to the matrix cores:
+ * Winograd-domain products, padded channels and partial tiles included -- the roofline numerator).
+ * Returns the number of entries (<= cap) or a negative error code. */
 int clasfv_kernel_timing(clasfv_t h, int cap, const char** names, int* launches, double* ms,
-                         double* gflop);
+                         double* gflop, double* xgflop);
 
 /* ---- clip plumbing: replaces src/fuse_utils.py:16-100 ----------------------------------------- */
 /* Build n clips (n,3,32,H,W) from the normalised video (3,T,H,W). Clip i is frames
@@ -97,8 +99,17 @@ int clasfv_build_clips(const float* video_dev, int T, int H, int W, const int32_
  * (labels_dev is (K,T,H,W) uint8). pass_clip0 is a host array of K ints. */
 int clasfv_pass_labels(const float* logits_dev, int K, const int32_t* pass_clip0, int T, int step, int H,
                        int W, int interpolate, uint8_t* labels_dev, void* stream);
-/* Per-frame label fusion over the K shifted passes (fuse_utils.py:82-100). Output (T',H,W) uint8
- * with T' = T - (step - 1). method: CLASFV_FUSE_MAJORITY or CLASFV_FUSE_SIMPLE. */
+/* Same labels from logit margins d = l1 - l0 ((n,32,H,W) per clip, clasfv_logit_margin) instead of
+ * the two logit planes: bit-identical, because the 2-class softmax depends on the logits only
+ * through fl(l1 - l0). Used for the multi-GPU exchange (half the bytes on xGMI). */
+int clasfv_pass_labels_margin(const float* margin_dev, int K, const int32_t* pass_clip0, int T, int step,
+                              int H, int W, int interpolate, uint8_t* labels_dev, void* stream);
+/* margin_dev (n,32,H,W) = logits_dev[:,1] - logits_dev[:,0] for n clips of (2,32,H,W) logits. */
+int clasfv_logit_margin(const float* logits_dev, int n, int H, int W, float* margin_dev, void* stream);
+/* Per-frame label fusion over the K <= 64 shifted passes (fuse_utils.py:82-100). Output (T',H,W)
+ * uint8 with T' = T - (step - 1). method: CLASFV_FUSE_MAJORITY, CLASFV_FUSE_SIMPLE or
+ * CLASFV_FUSE_STAPLE (LabelFusion's methods, fuse_utils.py:95; SIMPLE and STAPLE are restated from
+ * their papers: LabelFusion itself is absent, so their parity is unpinned). */
 int clasfv_fuse_votes(const uint8_t* labels_dev, int K, int T, int step, int H, int W, int method,
                       uint8_t* fused_dev, void* stream);
 
@@ -125,8 +136,11 @@ int clasfv_warp_backward(const float* grad_out_dev, const float* img_dev, int N,
  * video (bit-exact vs PyTorch's CPU kernel). Not normalised: follow with clasfv_zeroone_normalize. */
 int clasfv_preprocess_video(const uint8_t* frames_dev, int T, int Hs, int Ws, int H, int W, float* out_dev,
                             void* stream);
-/* In place: per channel c of video (3, n_per_channel) subtract the channel min, divide by the max. */
-int clasfv_zeroone_normalize(float* video_dev, int64_t n_per_channel, void* stream);
+/* In place: per channel c of video (3, n_per_channel) subtract the channel min, divide by the max.
+ * workspace_dev: caller-owned device scratch of clasfv_zeroone_workspace_bytes() bytes, used in
+ * stream order (concurrent calls on different streams need different workspaces). */
+int64_t clasfv_zeroone_workspace_bytes(void);
+int clasfv_zeroone_normalize(float* video_dev, int64_t n_per_channel, float* workspace_dev, void* stream);
 
 #ifdef __cplusplus
 }

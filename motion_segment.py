@@ -1,11 +1,13 @@
 """Drop-in for the reference CLI ``motion_segment.py`` (flags :19-65, outputs :117-150) on the
 MI355X engine: segment and motion-track the LV in an echo video, print EF, write pickles.
 
-Same flags and defaults, except:
-  * ``-d/--device`` defaults to ``cuda`` -- the engine runs on the GPU only (``cpu`` is rejected
-    with a clear error instead of silently falling back);
-  * extra opt-in flags: ``--synthetic-weights SEED`` (seeded random weights when no checkpoint is
-    available offline) and ``--batch-size`` (clips per forward call).
+Same flags and defaults. ``-d/--device`` keeps the reference default ``cpu``: there, as in the
+reference (whose ``nn.DataParallel`` scatters host tensors to GPU 0 whenever a GPU is visible,
+motion_segment.py:69-70), the video and the outputs live on the host and the engine runs on GPU 0 --
+a notice says so. There is no CPU compute path: without a GPU the CLI exits with an error.
+``-d cuda`` / ``cuda:i`` keep the video on that GPU end to end.
+Extra opt-in flags: ``--synthetic-weights SEED`` (seeded random weights when no checkpoint is
+available offline) and ``--batch-size`` (clips per forward call).
 Video input: any file OpenCV can decode if cv2 is installed (as the reference), or ``.npy`` holding
 (T,H,W,3) uint8 RGB frames.
 """
@@ -25,8 +27,8 @@ def parse_args(argv=None):
     ap.add_argument("-p", "--path", required=True, type=str, help="Path to the video")
     ap.add_argument("-m", "--model", required=False, type=str, help="Path to the saved model weights",
                     default="save_models/R2plus1DMotionSegNet_model.pth")
-    ap.add_argument("-d", "--device", required=False, type=str, help="Which device to use (GPU only: cuda[:i])",
-                    default="cuda")
+    ap.add_argument("-d", "--device", required=False, type=str, help="Which device to use: CPU or GPU",
+                    default="cpu")
     ap.add_argument("--fuse_method", required=False, type=str, help="Fuse method", default="simple")
     ap.add_argument("-f", "--fuse", required=False, type=int, help="Number of shifted video clips to fuse", default=1)
     ap.add_argument("-s", "--step", required=False, type=int, help="Step of shifting", default=1)
@@ -67,11 +69,19 @@ def read_video(path):
 
 def main(argv=None):
     args = parse_args(argv)
-    if not args.device.startswith("cuda"):
-        sys.exit("error: this engine runs on the GPU (MI355X); use -d cuda")
-    dev = torch.device(args.device)
-    if dev.index is None:
-        dev = torch.device("cuda", torch.cuda.current_device())
+    host_io = args.device.lower().startswith("cpu")
+    if not torch.cuda.is_available():
+        sys.exit("error: the CLAS-FV engine needs an MI355X (ROCm) GPU and none is visible")
+    if host_io:
+        print("notice: -d cpu: video and outputs stay in host memory; the engine runs on GPU 0 "
+              "(as the reference's DataParallel scatters host tensors to GPU 0)", file=sys.stderr)
+        dev = torch.device("cuda", 0)
+    else:
+        dev = torch.device(args.device)
+        if dev.type != "cuda":
+            sys.exit(f"error: unknown device {args.device!r}; use cpu, cuda or cuda:i")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
     torch.cuda.set_device(dev)
 
     from clasfv_amd.echo import compute_ef_using_putative_clips
@@ -81,7 +91,7 @@ def main(argv=None):
     from clasfv_amd.weights import DEFAULT_SEED, load_checkpoint
 
     seed = args.synthetic_weights if args.synthetic_weights is not None else DEFAULT_SEED
-    model = R2plus1D_18_MotionNet(pretrained=False, seed=seed)
+    model = R2plus1D_18_MotionNet(pretrained=False, seed=seed, device=dev)
     if args.synthetic_weights is None:
         model.load_state_dict(load_checkpoint(args.model))
     if args.verbose:
@@ -90,6 +100,8 @@ def main(argv=None):
 
     # motion_segment.py:96-106 on the device: uint8 frames -> resize -> zero-one normalisation
     video = preprocess_video(read_video(args.path), args.height, args.width, device=dev)
+    if host_io:  # the reference's -d cpu video is a host array handed to the (GPU) model clip by clip
+        video = video.cpu().numpy()
 
     segmentations = segment_a_video_with_fusion(video, model=model, interpolate_last=True, step=args.step,
                                                 num_clips=args.fuse, fuse_method=args.fuse_method, class_list=[0, 1],

@@ -12,8 +12,9 @@ numpy restatement of the reference clip plumbing and label fusion, ``src/fuse_ut
   being dropped for step > 1 (:85).
 * ``majority_vote`` / ``simple_vote`` -- the per-frame fusion rule. ``fuse_images`` lives in the
   unpinned, absent LabelFusion package: majority voting (ties -> lower label) is pinned only by the
-  golden fixtures produced with the same rule as a stub; SIMPLE is a restatement of the published
-  algorithm (Langerak et al. 2010, BraTS-toolkit form) and is **parity unpinned**.
+  golden fixtures produced with the same rule as a stub; SIMPLE (Langerak et al. 2010, BraTS-toolkit
+  form) and STAPLE (Warfield et al. 2004, ITK form) are restatements of the published algorithms and
+  are **parity unpinned**.
 """
 import numpy as np
 
@@ -173,6 +174,44 @@ def simple_vote(votes, class_list=(0, 1), t=0.05, stop=25, iterations=25):
     return result
 
 
+def staple_vote(votes, class_list=(0, 1), max_iter=100, tol=1e-7, init=0.99999):
+    """Binary STAPLE (Warfield, Zou & Wells 2004), in the form of ITK's STAPLEImageFilter: rater j's
+    decision D_j = (vote == 1); prior f = mean of all decisions; sensitivity p_j / specificity q_j
+    start at ``init``; E step W = f*P1 / (f*P1 + (1-f)*P0), P1 = prod_j (p_j if D_j else 1-p_j),
+    P0 = prod_j (1-q_j if D_j else q_j) (products in rater order, float64); M step p_j = sum W D_j /
+    sum W, q_j = sum (1-W)(1-D_j) / sum (1-W) (a zero denominator keeps the old value); stop when no
+    p_j, q_j moves by more than ``tol`` or after ``max_iter`` iterations; label 1 where W > 0.5.
+    ``fuse_images(..., "staple")`` of LabelFusion (src/fuse_utils.py:95) is absent: PARITY UNPINNED;
+    this is the restatement the GPU kernel (plumbing.hip fuse_staple_kernel) is checked against."""
+    d = np.stack([np.asarray(v) == 1 for v in votes]).reshape(len(votes), -1)
+    nv, npx = d.shape
+    f = d.sum() / float(nv * npx)
+    p = np.full(nv, init)
+    q = np.full(nv, init)
+
+    def e_step(p, q):
+        a = np.full(npx, f)
+        b = np.full(npx, 1.0 - f)
+        for j in range(nv):
+            a = a * np.where(d[j], p[j], 1.0 - p[j])
+            b = b * np.where(d[j], 1.0 - q[j], q[j])
+        s = a + b
+        with np.errstate(invalid="ignore", divide="ignore"):
+            return np.where(s > 0, a / s, f)
+
+    for _ in range(max_iter):
+        w = e_step(p, q)
+        sw = w.sum()
+        sn = npx - sw
+        np_ = np.array([(w * d[j]).sum() / sw if sw > 0 else p[j] for j in range(nv)])
+        nq_ = np.array([((1.0 - w) * ~d[j]).sum() / sn if sn > 0 else q[j] for j in range(nv)])
+        done = np.all(np.abs(np_ - p) <= tol) and np.all(np.abs(nq_ - q) <= tol)
+        p, q = np_, nq_
+        if done:
+            break
+    return (e_step(p, q) > 0.5).astype(np.uint8).reshape(np.asarray(votes[0]).shape)
+
+
 def _weighted_mv(cands, w):
     on = np.zeros(cands[0].shape, np.float64)
     off = np.zeros(cands[0].shape, np.float64)
@@ -183,7 +222,7 @@ def _weighted_mv(cands, w):
 
 
 FUSERS = {"majority": majority_vote, "majorityvoting": majority_vote, "mv": majority_vote,
-          "itkvoting": majority_vote, "simple": simple_vote}
+          "itkvoting": majority_vote, "simple": simple_vote, "staple": staple_vote}
 
 
 def fuse_frames(passes, t, step, fuse_method="simple", class_list=(0, 1)):

@@ -535,3 +535,154 @@ def test_wino_f2x4_matches_f2x2(model, monkeypatch, shape):
         import clasfv_amd.weights as W
         rs, rm = R.forward(W.synthetic_state_dict(W.DEFAULT_SEED), x.cpu().numpy())
         np.testing.assert_allclose(s_r.cpu().numpy(), rs.numpy(), rtol=0, atol=3e-3)
+
+
+# ---- north_star bar on BASELINE config[1] (round 2) -----------------------------------------------
+
+def _northstar():
+    import clasfv_amd.synthetic as S
+    g = golden("northstar_c1.npz")
+    video = fuse_ref.zeroone_normalizer(S.echo_video(int(g["T"]), seed=int(g["seed"])))
+    return g, video
+
+
+def test_northstar_config1_pass_labels_vs_cpu(model):
+    """Config[1] (200 frames, 5 shifted passes, 30 clips) through the real HIP model: every pass's
+    label video (clips built on the GPU, batched forward, softmax -> resample -> argmax) against the
+    CPU reference path (oracle model + numpy plumbing, tests/golden/make_golden_northstar.py)."""
+    from clasfv_amd import fuse_utils as FU
+    g, video = _northstar()
+    T, F, step = int(g["T"]), int(g["fuse"]), int(g["step"])
+    v = torch.from_numpy(video).cuda()
+    k = FU.clamp_num_clips(T, F, step)
+    table, clip0 = FU.clip_table(T, k, step)
+    labels = FU.pass_labels(FU.run_model(model, FU.build_clips(v, table)), clip0, T, step).cpu().numpy()
+    frames = g["pass_frames"]
+    ref_all = np.unpackbits(g["passes"])[: int(frames.sum()) * 112 * 112]
+    at = 0
+    for j, n in enumerate(frames):
+        ref = ref_all[at: at + n * 112 * 112].reshape(n, 112, 112)
+        at += n * 112 * 112
+        got = labels[j, :n]
+        assert dice_delta(got, ref) <= DICE_TOL, j
+        assert (got != ref).mean() <= 1e-4, j
+
+
+@pytest.mark.parametrize("method", ["majority", "simple", "staple"])
+def test_northstar_config1_fused_masks_and_ef_vs_cpu(model, method):
+    """north_star bar (BASELINE.json): fused masks Dice delta <= 1e-3 and EF within 1e-3 of the CPU
+    reference path, on config[1] with the real HIP model, through the drop-in
+    segment_a_video_with_fusion (src/fuse_utils.py:36-100) and compute_ef_using_putative_clips
+    (src/fuse_utils.py:105-148). SIMPLE / STAPLE fusion: the CPU side is the oracle restatement
+    (LabelFusion absent: parity with LabelFusion itself unpinned)."""
+    from clasfv_amd import fuse_utils as FU
+    from clasfv_amd.echo import compute_ef_using_putative_clips
+    g, video = _northstar()
+    out = FU.segment_a_video_with_fusion(video, model, num_clips=int(g["fuse"]), step=int(g["step"]),
+                                         fuse_method=method)
+    shp = tuple(g[f"fused_{method}_shape"])
+    ref = np.unpackbits(g[f"fused_{method}"])[: int(np.prod(shp))].reshape(shp).astype(np.int64)
+    assert out.dtype == np.int64 and out.shape == ref.shape
+    assert dice_delta(out, ref) <= DICE_TOL
+    efs, pairs = compute_ef_using_putative_clips(out, "gpu", return_edes=True)
+    assert np.array(pairs, np.int64).reshape(-1, 2).tolist() == g[f"pairs_{method}"].tolist()
+    np.testing.assert_allclose(np.array(efs, np.float64), g[f"ef_{method}"], rtol=0, atol=1e-3, equal_nan=True)
+
+
+@pytest.mark.parametrize("K,T,step", [(3, 30, 1), (5, 40, 1), (17, 60, 1), (6, 50, 3), (40, 80, 1)])
+def test_fuse_staple_vs_oracle(K, T, step):
+    """STAPLE fusion kernel vs the oracle restatement (same iteration; float64 reductions in a
+    different order, so a pixel whose posterior is within rounding of 0.5 could differ)."""
+    from clasfv_amd import fuse_utils as FU
+    passes = _noisy_passes(K, T, step, seed=K * 7 + T)
+    labels = np.zeros((K, T) + passes[0].shape[1:], np.uint8)
+    for k, p in enumerate(passes):
+        labels[k, :p.shape[0]] = p
+    got = FU.fuse_votes(torch.from_numpy(labels).cuda(), step, "staple").cpu().numpy()
+    ref = fuse_ref.fuse_frames(passes, T, step, "staple")
+    assert got.shape == ref.shape
+    assert (got != ref).mean() <= 1e-5
+
+
+@pytest.mark.parametrize("method", ["simple", "majority"])
+def test_fuse_40_passes(method):
+    """The reference accepts any num_clips (-f 40): K up to 64 passes."""
+    from clasfv_amd import fuse_utils as FU
+    K, T, step = 40, 70, 1
+    passes = _noisy_passes(K, T, step, seed=404)
+    labels = np.zeros((K, T) + passes[0].shape[1:], np.uint8)
+    for k, p in enumerate(passes):
+        labels[k, :p.shape[0]] = p
+    got = FU.fuse_votes(torch.from_numpy(labels).cuda(), step, method).cpu().numpy()
+    np.testing.assert_array_equal(got, fuse_ref.fuse_frames(passes, T, step, method))
+
+
+def test_pipeline_f40_runs_like_reference():
+    from clasfv_amd import fuse_utils as FU
+    v = _norm_video(120, 9)
+    for meth in ("majority", "simple"):
+        def np_model(x):
+            s, m = fake_model(torch.from_numpy(np.ascontiguousarray(x)))
+            return s.numpy(), m.numpy()
+        out = FU.segment_a_video_with_fusion(v, fake_model, num_clips=40, fuse_method=meth)
+        ref = fuse_ref.segment_a_video_with_fusion(v, np_model, num_clips=40, fuse_method=meth)
+        np.testing.assert_array_equal(out, ref)
+
+
+@pytest.mark.parametrize("T,step", [(70, 1), (96, 2), (200, 1)])
+def test_pass_labels_from_margins_bitexact(T, step):
+    """The multi-GPU exchange payload: labels from the logit margin l1 - l0 equal labels from both
+    logit planes bit for bit (including resampled passes and near-tie logits)."""
+    from clasfv_amd import fuse_utils as FU
+    k = FU.clamp_num_clips(T, 4, step)
+    table, clip0 = FU.clip_table(T, k, step)
+    rng = np.random.default_rng(T)
+    lg = rng.normal(0, 2, (len(table), 2, 32, 40, 48)).astype(np.float32)
+    lg[:, 1, :, :4] = lg[:, 0, :, :4]                                   # exact ties
+    lg[:, 1, :, 4:8] = np.nextafter(lg[:, 0, :, 4:8], np.float32(np.inf))  # 1-ulp margins
+    logits = torch.from_numpy(lg).cuda()
+    a = FU.pass_labels(logits, clip0, T, step)
+    m = FU.logit_margin(logits)
+    assert torch.equal(m, logits[:, 1] - logits[:, 0])
+    b = FU.pass_labels(m, clip0, T, step, margin=True)
+    assert torch.equal(a, b)
+
+
+def test_cli_default_device_cpu_matches_cuda(tmp_path):
+    """Reference default -d cpu: host video and outputs, engine on GPU 0, same masks as -d cuda."""
+    import pickle
+    import subprocess
+    import sys
+    import clasfv_amd.synthetic as S
+    vid = tmp_path / "echo_dev.npy"
+    np.save(vid, S.echo_video_uint8(90, seed=6))
+    outs = {}
+    for dev in (None, "cuda"):
+        d = tmp_path / (dev or "default")
+        d.mkdir()
+        cmd = [sys.executable, "motion_segment.py", "-p", str(vid), "--synthetic-weights", "1234", "-f", "3",
+               "-c", "binary_video", "-o", str(d)] + (["-d", dev] if dev else [])
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        if dev is None:
+            assert "engine runs on GPU 0" in r.stderr
+        outs[dev] = pickle.load(open(d / "echo_dev_whole_video_segmentation.pkl", "rb"))
+    assert outs[None].dtype == np.int64 and np.array_equal(outs[None], outs["cuda"])
+
+
+def test_normalizer_workspace_per_call_streams():
+    """The normaliser's partials live in a caller-owned workspace (no shared static buffer): two
+    videos normalised on two streams give the single-stream results."""
+    from clasfv_amd.preprocess import zeroone_normalize_
+    import clasfv_amd.synthetic as S
+    a = torch.from_numpy(S.echo_video(64, seed=1)).cuda()
+    b = torch.from_numpy(S.echo_video(64, seed=2)).cuda() * 0.5 + 3
+    ra, rb = zeroone_normalize_(a.clone()), zeroone_normalize_(b.clone())
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        xa = zeroone_normalize_(a.clone())
+    with torch.cuda.stream(s2):
+        xb = zeroone_normalize_(b.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(xa, ra) and torch.equal(xb, rb)

@@ -178,37 +178,74 @@ def test_clip_shard_all_gather_gloo(world, n_total):
         np.testing.assert_array_equal(res[r], ref)
 
 
+def _plans(sizes):
+    out, off = [], 0
+    for n in sizes:
+        out.append({"n": n, "offset": off})
+        off += n
+    return out
+
+
 def _owner_worker(rank, world, port, sizes, q):
     import torch.distributed as dist
-    from clasfv_amd.dist import exchange_to_owners, shard_bounds
+    from clasfv_amd.dist import exchange_to_owners, owner_of_clips, shard_bounds
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        owners = [vi % world for vi, n in enumerate(sizes) for _ in range(n)]
+        owners = owner_of_clips(_plans(sizes), world)
         lo, hi = shard_bounds(len(owners), rank, world)
         local = torch.arange(lo, hi, dtype=torch.float32)[:, None] * torch.ones(1, 3)  # row g = g
-        q.put((rank, exchange_to_owners(local, owners, rank, world).numpy()))
+        got = exchange_to_owners(local, owners, rank, world)
+        q.put((rank, got.numpy(), got.data_ptr() == local.data_ptr()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,sizes", [(2, [6, 5, 7]), (3, [1, 1, 1, 1, 1]), (2, [30, 30]), (3, [4, 0, 9, 2])])
+@pytest.mark.parametrize("world,sizes", [(2, [6, 5, 7]), (3, [1, 1, 1, 1, 1]), (2, [30, 30]), (3, [4, 0, 9, 2]),
+                                         (2, [30] * 16), (3, [7, 30, 2, 30, 11])])
 def test_owner_exchange_gloo(world, sizes):
     """Owner exchange (all_to_all of per-clip rows to the rank fusing their video): every rank gets
-    exactly the rows of the videos it owns, in global order; the one-video-per-rank case moves nothing."""
+    exactly the rows of the videos it owns (video_owners), in global order; when every video lies in
+    one rank's block (e.g. 8 equal videos per rank) nothing moves and each rank keeps its own rows."""
     import torch.multiprocessing as mp
+    from clasfv_amd.dist import rows_exchanged, owner_of_clips, video_owners
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_owner_worker, args=(r, world, port, sizes, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(world))
+    res = {}
+    for _ in range(world):
+        r, rows, same = q.get(timeout=120)
+        res[r] = (rows, same)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
     offs = np.cumsum([0] + sizes)
+    vown = video_owners(_plans(sizes), world)
+    moved = rows_exchanged(owner_of_clips(_plans(sizes), world), world)
     for r in range(world):
-        want = np.concatenate([np.arange(offs[v], offs[v + 1]) for v in range(len(sizes)) if v % world == r] or
+        want = np.concatenate([np.arange(offs[v], offs[v + 1]) for v in range(len(sizes)) if vown[v] == r] or
                               [np.zeros(0)]).astype(np.float32)
-        np.testing.assert_array_equal(res[r][:, 0], want)
+        np.testing.assert_array_equal(res[r][0][:, 0], want)
+        if moved == 0 and len(want):
+            assert res[r][1], "no exchange: the rank's own rows are returned as they are"
+    if sizes == [30] * 16:
+        assert moved == 0
+
+
+def test_owner_mapping_is_block_aligned():
+    """SURVEY 8(e) / config[2]: 64 equal videos over 8 ranks (and 8 per rank over 2) exchange no
+    clip; a straddling video is owned by the rank holding most of its clips."""
+    from clasfv_amd.dist import owner_of_clips, rows_exchanged, video_owners
+    for world, n_vid in ((8, 64), (2, 16), (4, 64), (8, 8), (1, 5)):
+        plans = _plans([30] * n_vid)
+        assert rows_exchanged(owner_of_clips(plans, world), world) == 0
+        assert video_owners(plans, world) == [v * world // n_vid for v in range(n_vid)]
+    # 3 videos of 30 clips over 2 ranks: blocks [0,45), [45,90) -> video 1 straddles 15/15 -> rank 0
+    plans = _plans([30, 30, 30])
+    assert video_owners(plans, 2) == [0, 0, 1]
+    assert rows_exchanged(owner_of_clips(plans, 2), 2) == 15
+    plans = _plans([10, 40, 10])  # blocks [0,30), [30,60): video 1 has 20 clips in rank 0, 20 in 1 -> 0
+    assert video_owners(plans, 2) == [0, 0, 1]

@@ -178,3 +178,23 @@ def test_warp_backward_oracle_matches_reference():
     np.testing.assert_array_equal(out.detach().numpy(), g["warp_out"])
     np.testing.assert_array_equal(mot.grad.numpy(), g["warp_grad_motion"])
     np.testing.assert_array_equal(img.grad.numpy(), g["warp_grad_img"])
+
+
+def test_staple_restatement_known_answers():
+    """STAPLE (parity unpinned: LabelFusion absent) -- properties of the published algorithm:
+    unanimous raters are reproduced; a rater that disagrees with the others everywhere gets low
+    sensitivity/specificity and is outvoted; the output is a binary uint8 image of the input shape."""
+    from oracle import fuse_ref
+    rng = np.random.default_rng(0)
+    truth = rng.integers(0, 2, (40, 48)).astype(np.uint8)
+    assert np.array_equal(fuse_ref.staple_vote([truth] * 3), truth)
+    noisy = [truth.copy() for _ in range(4)]
+    for v in noisy[:3]:  # three good raters with 3 % independent flips
+        flip = rng.uniform(size=truth.shape) < 0.03
+        v[flip] ^= 1
+    noisy[3] = 1 - truth  # an adversarial rater
+    out = fuse_ref.staple_vote(noisy)
+    assert out.dtype == np.uint8 and out.shape == truth.shape
+    assert (out != truth).mean() < 0.01
+    assert np.array_equal(fuse_ref.staple_vote([np.zeros((5, 5), np.uint8)] * 2), np.zeros((5, 5), np.uint8))
+    assert np.array_equal(fuse_ref.staple_vote([np.ones((5, 5), np.uint8)] * 2), np.ones((5, 5), np.uint8))
