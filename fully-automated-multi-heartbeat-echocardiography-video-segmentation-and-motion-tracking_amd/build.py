@@ -16,6 +16,9 @@ LIB_PATH = os.path.join(PKG_DIR, "libclasfv.so")
 SOURCES = ["engine.hip", "conv.hip", "conv_patch.hip", "winograd.hip", "winograd2.hip", "winograd3.hip", "winograd_t.hip", "decoder.hip", "plumbing.hip"]
 HEADERS = ["common.h", "plumbing.h"]
 ARCH = os.environ.get("CLASFV_OFFLOAD_ARCH", "gfx950")
+# Per-file extra flags. winograd_t.hip: no SLP vectorisation -- packed f32 VALU (v_pk_*) beside
+# MFMAs costs issue cycles and the pack/unpack moves doubled the temporal kernel's vector stream.
+EXTRA_FLAGS = {"winograd_t.hip": ["-fno-slp-vectorize"]}
 
 
 def _hipcc():
@@ -52,7 +55,7 @@ def build(force=False, verbose=False):
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
-        cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [hipcc] + flags + EXTRA_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)

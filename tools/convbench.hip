@@ -4,6 +4,7 @@
 //   KIND: wino (1x3x3 s1), winot (3x1x1 s1), sp (1x3x3 direct), tp (3x1x1 direct), pw (1x1x1)
 // KO = knock-out variant of the Winograd kernels (see winograd.hip): timing only, results are wrong.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -104,6 +105,20 @@ int main(int argc, char** argv) {
   p.x = bf ? to_bf16_dev(nx, 0.f, 1.f, 1) : dev_random(nx, 0.f, 1.f, 1);
   const size_t nw = winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
   p.w = bf ? to_bf16_dev(nw, -0.05f, 0.05f, 2) : dev_random(nw, -0.05f, 0.05f, 2);
+  if (winot) {  // conv_winot3's layout of the same U values (winot3_transform_weights)
+    std::vector<float> hu(nw), hu3(nw);
+    CK(hipMemcpy(hu.data(), p.w, nw * 4, hipMemcpyDeviceToHost));
+    for (int k = 0; k < Cin / 8; ++k)
+      for (int e = 0; e < 6; ++e)
+        for (int o = 0; o < Cout; ++o)
+          for (int c8 = 0; c8 < 8; ++c8)
+            hu3[(((((size_t)k * 3 + e / 2) * Cout + o) * 4 + c8 / 2) * 2 + e % 2) * 2 + c8 % 2] =
+                hu[(((size_t)k * 6 + e) * Cout + o) * 8 + c8];
+    void* d;
+    CK(hipMalloc(&d, nw * 4));
+    CK(hipMemcpy(d, hu3.data(), nw * 4, hipMemcpyHostToDevice));
+    p.w_alt = d;
+  }
   p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
   p.res = getenv("CB_NORES") ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
   CK(hipMalloc(&p.y, ny * 4));
@@ -148,6 +163,30 @@ int main(int argc, char** argv) {
   for (size_t v = 0; v < kos.size(); ++v)
     printf("%s%s%-6s N=%d T=%d H=%d W=%d Cin=%d Cout=%d ko=%-3d  %8.3f ms  %7.1f TF(alg)\n", p.res ? "res   " : "nores ", bf ? "bf16 " : "",
            kind, N, T, H, W, Cin, Cout, kos[v], best[v], gflop / best[v]);
+  // CB_CHECK=1: every variant's output against the first one's (bitwise; max |diff| printed)
+  if (getenv("CB_CHECK") && kos.size() > 1) {
+    std::vector<float> ref(ny), got(ny);
+    CK(hipMemset(p.y, 0, ny * 4));
+    launch(kos[0]);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(ref.data(), p.y, ny * 4, hipMemcpyDeviceToHost));
+    for (size_t v = 1; v < kos.size(); ++v) {
+      CK(hipMemset(p.y, 0, ny * 4));
+      launch(kos[v]);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(got.data(), p.y, ny * 4, hipMemcpyDeviceToHost));
+      size_t nd = 0;
+      double md = 0;
+      for (size_t i = 0; i < ny; ++i)
+        if (got[i] != ref[i]) {
+          ++nd;
+          const double d = fabs((double)got[i] - (double)ref[i]);
+          if (d > md || d != d) md = d;
+        }
+      printf("check ko=%d vs ko=%d: %zu of %zu differ, max |diff| %.3e%s\n", kos[v], kos[0], nd, ny, md,
+             nd ? "" : " (bit-identical)");
+    }
+  }
   return 0;
 }
 

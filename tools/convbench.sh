@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/.."
 C=fully-automated-multi-heartbeat-echocardiography-video-segmentation-and-motion-tracking_amd/csrc
 mkdir -p gpurun_out
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -DCLASFV_KNOCKOUTS -Iinclude -o gpurun_out/convbench \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -DCLASFV_KNOCKOUTS -Iinclude -o ${CB_OUT:-gpurun_out/convbench} \
   tools/convbench.hip $C/winograd.hip $C/winograd2.hip $C/winograd3.hip $C/winograd_t.hip $C/conv.hip $C/conv_patch.hip $C/decoder.hip
 [ "$1" = build ] && exit 0
 B=gpurun_out/convbench
