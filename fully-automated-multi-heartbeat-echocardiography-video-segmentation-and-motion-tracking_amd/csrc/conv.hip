@@ -18,7 +18,10 @@
 //    exactly the lane's 8-element operand. fp32 accumulation either way;
 //  * 1-D grid with an XCD-aware swizzle, N tiles fastest: the blocks re-reading one A tile (and the
 //    3x3 halo rows of their neighbours) share an XCD's L2;
-//  * epilogue: folded-BN bias, residual add, ReLU, fp32 or bf16 store.
+//  * the MFMAs compute D^T = W . A^T (weights as the A operand): an accumulator lane then holds 4
+//    CONSECUTIVE output channels of one voxel, so the epilogue (folded-BN bias, residual add, ReLU)
+//    moves 16-B fp32 / 8-B bf16 vectors instead of one element per lane (same products, same
+//    accumulation order: bit-identical to the untransposed form).
 #include <hip/hip_bf16.h>
 #include <stdlib.h>
 
@@ -33,44 +36,45 @@ __device__ inline int xcd_swizzle(int b, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
-__device__ inline float load_res(const void* res, size_t o, int bf16) {
-  return bf16 ? (float)reinterpret_cast<const __bf16*>(res)[o] : reinterpret_cast<const float*>(res)[o];
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ inline f32x4 load_res4(const void* res, size_t o, int bf16) {
+  if (bf16) {
+    const bf16x4 v = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const __bf16*>(res) + o);
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  }
+  return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(res) + o);
 }
 
-__device__ inline void store_out(void* y, size_t o, float v, int bf16) {
+__device__ inline void store_out4(void* y, size_t o, f32x4 v, int bf16) {
   if (bf16)
-    reinterpret_cast<__bf16*>(y)[o] = (__bf16)v;
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(y) + o) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
   else
-    reinterpret_cast<float*>(y)[o] = v;
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(y) + o) = v;
 }
 
+// acc[i][j] (D^T layout): lane (l16, q) holds channels n0 + 16j + 4q .. +3 of voxel m_base + 16i + l16.
+// Cout is a multiple of 16, so a 4-channel group is either all inside or all outside. Each lane
+// reads its residual vector before writing the same addresses (res may alias y).
 template <int MT, int NT>
 __device__ inline void epilogue(const ConvParams& p, const f32x4 (&acc)[MT][NT], int m_base, int n0, int q, int l16) {
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int n = n0 + j * 16 + l16;
-    if (n >= p.Cout) continue;
-    const float bv = p.bias ? p.bias[n] : 0.f;
-    // the residual values of this column are all loaded before any store (res may alias y, so a
-    // load after a store would have to wait for it)
-    float rv[MT][4];
+  for (int i = 0; i < MT; ++i) {
+    const int m = m_base + i * 16 + l16;
+    if (m >= p.M) continue;
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+    for (int j = 0; j < NT; ++j) {
+      const int n = n0 + j * 16 + 4 * q;
+      if (n >= p.Cout) continue;
+      const size_t o = (size_t)m * p.Cout + n;
+      const f32x4 bv = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 rv = p.res ? load_res4(p.res, o, p.out_bf16) : f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 v = acc[i][j] + bv + rv;
+      if (p.relu) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m_base + i * 16 + q * 4 + r;
-        rv[i][r] = (p.res && m < p.M) ? load_res(p.res, (size_t)m * p.Cout + n, p.out_bf16) : 0.f;
+        for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.f);
       }
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m_base + i * 16 + q * 4 + r;
-        if (m >= p.M) continue;
-        float v = acc[i][j][r] + bv + rv[i][r];
-        if (p.relu) v = fmaxf(v, 0.f);
-        store_out(p.y, (size_t)m * p.Cout + n, v, p.out_bf16);
-      }
+      store_out4(p.y, o, v, p.out_bf16);
     }
   }
 }
@@ -204,7 +208,7 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles) {
         for (int i = 0; i < MT; ++i)
 #pragma unroll
           for (int j = 0; j < NT; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][kk], b[j][kk], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j][kk], a[i][kk], acc[i][j], 0, 0, 0);
     } else {
       bf16x8 a[MT], b[NT];
 #pragma unroll
@@ -214,7 +218,7 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles) {
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
     }
   }
   epilogue<MT, NT>(p, acc, m0 + wid * 16 * MT, n0, q, l16);
@@ -314,7 +318,7 @@ __global__ __launch_bounds__(256) void conv_stem_f32(ConvParams p, int n_tiles) 
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][kk], b[j][kk], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j][kk], a[i][kk], acc[i][j], 0, 0, 0);
     if (more) store_tiles(cur ^ 1);
     __syncthreads();
     cur ^= 1;

@@ -17,8 +17,9 @@
 //  * counted vmcnt: at step s a wave waits for its own B(s) (and, implied by in-order completion,
 //    the patch of the step's chunk), then a block barrier; the next chunk's patch is issued at the
 //    chunk's tap 0, after the barrier that retires the buffer's previous chunk;
-//  * epilogue: folded-BN bias, optional residual, ReLU, bf16 stores; voxels outside the map (ragged
-//    28/14/7-pixel maps) are masked.
+//  * epilogue: the MFMAs compute D^T = W . A^T, so a lane holds 4 consecutive output channels of
+//    one voxel: folded-BN bias, optional residual, ReLU, 8-B bf16 stores; voxels outside the map
+//    (ragged 28/14/7-pixel maps) are masked.
 #include <hip/hip_bf16.h>
 #include <stdlib.h>
 
@@ -168,42 +169,36 @@ __global__ __launch_bounds__(256) void conv_patch_bf16(ConvParams p, int n_tiles
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
   }
 
-  // epilogue: accumulator row 4q + r of fragment i is tile voxel 32*wid + 16*i + 4q + r
-  size_t gm[2][4];
-  bool ok[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = wid * 32 + i * 16 + q * 4 + r;
-      const int to = t0 + (m >> 6), ho = h0 + ((m >> 3) & 7), wo = w0 + (m & 7);
-      ok[i][r] = to < p.To && ho < p.Ho && wo < p.Wo;
-      gm[i][r] = (((size_t)nclip * p.To + to) * p.Ho + ho) * p.Wo + wo;
-    }
+  // epilogue: accumulator acc[i][j] holds channels n0 + 16j + 4q .. +3 of tile voxel 32*wid + 16*i + l16
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   const __bf16* res = reinterpret_cast<const __bf16*>(p.res);
   __bf16* y = reinterpret_cast<__bf16*>(p.y);
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int n = n0 + j * 16 + l16;
-    if (n >= p.Cout) continue;
-    const float bv = p.bias ? p.bias[n] : 0.f;
-    float rv[2][4];
+  for (int i = 0; i < 2; ++i) {
+    const int m = wid * 32 + i * 16 + l16;
+    const int to = t0 + (m >> 6), ho = h0 + ((m >> 3) & 7), wo = w0 + (m & 7);
+    if (!(to < p.To && ho < p.Ho && wo < p.Wo)) continue;
+    const size_t gm = (((size_t)nclip * p.To + to) * p.Ho + ho) * p.Wo + wo;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) rv[i][r] = (res && ok[i][r]) ? (float)res[gm[i][r] * p.Cout + n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (!ok[i][r]) continue;
-        float v = acc[i][j][r] + bv + rv[i][r];
-        if (p.relu) v = fmaxf(v, 0.f);
-        y[gm[i][r] * p.Cout + n] = (__bf16)v;
+    for (int j = 0; j < NT; ++j) {
+      const int n = n0 + j * 16 + 4 * q;
+      if (n >= p.Cout) continue;
+      const size_t o = gm * p.Cout + n;
+      f32x4 v = acc[i][j];
+      if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
+      if (res) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + o);
+        v += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
       }
+      if (p.relu) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.f);
+      }
+      *reinterpret_cast<bf16x4*>(y + o) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    }
   }
 }
 
