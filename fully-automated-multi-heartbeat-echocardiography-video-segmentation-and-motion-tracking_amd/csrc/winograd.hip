@@ -38,12 +38,10 @@ __device__ inline int xcd_swizzle_w(int b, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
-// KO != 0 only in tools/convbench.hip (knock-out timing builds): bit 1 no transform, 2 no raw DMA,
-// 4 no U loads, 8 no epilogue, 16 no MFMA.
 // NCH > 0: the chunk count Cin/8 as a compile-time constant -> the chunk loop is fully unrolled and
 // the compiler's own vmcnt waits are exact (the runtime loop makes it wait for the previous chunk's
 // fetches too, one chunk early).
-template <int NT, int KO = 0, int NCH = 0>
+template <int NT, int NCH = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino(ConvParams p, int n_co,
                                                                                              int n_tiles) {
   __shared__ __align__(16) char smem[RAW_STAGES * RAW_BYTES + 2 * V_BYTES];
@@ -78,7 +76,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     d_off[j] = off;
   }
   auto issue_raw = [&](int chunk, int buf) {
-    if constexpr (KO & 2) return;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const void* src = (d_off[j] >= 0 && chunk >= 0) ? (const void*)(x + (size_t)d_off[j] + chunk * 8) : p.zero;
@@ -93,17 +90,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // The transform is split so that the raw reads of chunk k+1 are issued before the MFMAs of chunk
   // k and its arithmetic + V stores fill their issue gaps (sched_group_barrier in step()).
   auto transform_read = [&](int buf_raw, float (&d)[16]) {
-    if constexpr (KO & 1) {
-#pragma unroll
-      for (int i2 = 0; i2 < 16; ++i2) d[i2] = (float)(buf_raw + i2);
-      return;
-    }
     const float* rb = reinterpret_cast<const float*>(raw + buf_raw * RAW_BYTES) + tt * 128 + cc;
 #pragma unroll
     for (int px = 0; px < 16; ++px) d[px] = rb[(px ^ (tt & 7)) * 8];
   };
   auto transform_write = [&](const float (&d)[16], int buf_v) {
-    if constexpr (KO & 1) return;
     float t[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {  // B^T d
@@ -130,11 +121,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float* ub = U + (((size_t)wid * CO + n0 + l16) * 4 + q) * 8;
   f32x4 u0[NT][2], u1[NT][2], u2[NT][2];
   auto load_u = [&](int chunk, f32x4 (&u)[NT][2]) {
-    if constexpr (KO & 4) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) u[nt][0] = u[nt][1] = f32x4{1.f, 1.f, 1.f, 1.f} * (float)chunk;
-      return;
-    }
     const float* b = ub + (size_t)chunk * 4 * CO * 32;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -203,26 +189,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) {
-            if constexpr (KO & 16)
-              acc[j][m][nt][0] += a[j][2 * m + s] * uc[nt][j >> 1][(j & 1) * 2 + s];
-            else
-              acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][2 * m + s], uc[nt][j >> 1][(j & 1) * 2 + s],
-                                                                   acc[j][m][nt], 0, 0, 0);
+            acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][2 * m + s], uc[nt][j >> 1][(j & 1) * 2 + s],
+                                                                 acc[j][m][nt], 0, 0, 0);
           }
     transform_write(d, (k + 1) & 1);
-    if constexpr (KO == 0) {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
-      }
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
     }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
   };
   if constexpr (NCH > 0) {
 #pragma unroll
@@ -246,17 +227,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // ---- epilogue: Y = A^T M A. Wave i holds row i of M: the column combination (. A) is done in
   // registers, Z_i = (M_i0 + M_i1 + M_i2, M_i1 - M_i2 - M_i3); the row combination (A^T .) needs all
   // four waves and goes through LDS: Z[i][tile][co][2] (48 KB), one barrier.
-  if constexpr ((KO & 8) != 0) {
-    float sink = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) sink += acc[j][m][nt][0] + acc[j][m][nt][3];
-    if (sink == 1.2345f) reinterpret_cast<float*>(p.y)[tid] = sink;
-    return;
-  }
   // Unit = (tile, 4 consecutive channels): 16-B bias / residual loads and 16-B stores. All of a
   // thread's global loads are issued before the LDS exchange (their latency hides behind it, and
   // res may alias y: no load can then wait behind a store).
@@ -352,31 +322,20 @@ hipError_t launch_wino(const ConvParams& p, hipStream_t s) {
   const int n_co = p.Cout / 48;
   const int nb = (n_tiles + BT - 1) / BT;
   switch (p.Cin >> 3) {  // fully unrolled chunk loops for the layer1 / layer2 widths
-    case 8: hipLaunchKernelGGL((conv_wino<3, 0, 8>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
-    case 16: hipLaunchKernelGGL((conv_wino<3, 0, 16>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
-    default: hipLaunchKernelGGL((conv_wino<3, 0, 0>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 8: hipLaunchKernelGGL((conv_wino<3, 8>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
+    case 16: hipLaunchKernelGGL((conv_wino<3, 16>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
+    default: hipLaunchKernelGGL((conv_wino<3, 0>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
   }
   return hipGetLastError();
 }
 
 #ifdef CLASFV_KNOCKOUTS
+// tools/convbench.hip: 0 = product dispatch, 100 = the runtime-chunk-loop instance
 hipError_t launch_wino_ko(const ConvParams& p, hipStream_t s, int ko) {
+  if (ko != 100) return launch_wino(p, s);
   const int n_tiles = p.N * p.To * ((p.Ho + 1) / 2) * ((p.Wo + 1) / 2);
   const int n_co = p.Cout / 48;
-  const dim3 g(((n_tiles + BT - 1) / BT) * n_co);
-  switch (ko) {
-    case 0: return launch_wino(p, s);
-    case 100: hipLaunchKernelGGL((conv_wino<3, 0>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
-    case 1: hipLaunchKernelGGL((conv_wino<3, 1>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
-    case 2: hipLaunchKernelGGL((conv_wino<3, 2>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
-    case 4: hipLaunchKernelGGL((conv_wino<3, 4>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
-    case 8: hipLaunchKernelGGL((conv_wino<3, 8>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
-    case 16: hipLaunchKernelGGL((conv_wino<3, 16>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
-    case 7: hipLaunchKernelGGL((conv_wino<3, 7>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
-    case 15: hipLaunchKernelGGL((conv_wino<3, 15>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
-    case 6: hipLaunchKernelGGL((conv_wino<3, 6>), g, dim3(256), 0, s, p, n_co, n_tiles); break;
-    default: return hipErrorInvalidValue;
-  }
+  hipLaunchKernelGGL((conv_wino<3, 0>), dim3(((n_tiles + BT - 1) / BT) * n_co), dim3(256), 0, s, p, n_co, n_tiles);
   return hipGetLastError();
 }
 #endif

@@ -34,9 +34,9 @@ __device__ inline void dma16(const void* src, void* lds_dst) {
 // raw ring 3 x 8 KB, V ring 3 x 16 KB so that each chunk's V operands are read into registers one
 // chunk ahead (2-way rotation) and the MFMAs start right after the chunk barrier (2.51 -> 2.43 ms on
 // layer1). One barrier per chunk.
-// Knock-out probes (tools/convbench.sh): U operands replaced by lane-varying register values cost
-// the same as the loads (KO 128), and loading chunk 0's U every chunk (L1-resident, KO 64) is no
-// faster: the U fetch is not a bottleneck; the MFMA issue stream itself is (SQ_VALU_MFMA_BUSY 57 %).
+// Timing probes (round 1): U operands replaced by lane-varying register values cost the same as the
+// loads, and loading chunk 0's U every chunk (L1-resident) is no faster: the U fetch is not a
+// bottleneck; the MFMA issue stream itself is (SQ_VALU_MFMA_BUSY 57 %).
 constexpr int Q_BT = 32;
 constexpr int Q_V = 16 * Q_BT * 32;   // 16 KB
 
@@ -59,7 +59,7 @@ struct QPatch {
 static_assert(QPatch<4>::LDS == 72 * 1024 && QPatch<4>::DPW == 2, "PT = 4 layout");
 static_assert(QPatch<2>::DPW == 3 && QPatch<2>::LDS <= 80 * 1024, "PT = 2 layout: 2 blocks per CU");
 
-template <int NCH, int KO = 0, int PT = 4>
+template <int NCH, int PT = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino_q(ConvParams p, int n_co,
                                                                                              int n_patches) {
   using G = QPatch<PT>;
@@ -100,12 +100,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     d_off[j] = off;
   }
   auto issue_raw = [&](int k, int stage) __attribute__((always_inline)) {
-    if constexpr (KO & 2) return;
 #pragma unroll
     for (int j = 0; j < DPW; ++j) {
       const void* src = (k < nchunk && d_off[j] >= 0) ? (const void*)(x + (size_t)d_off[j] + k * 8) : p.zero;
-      if constexpr ((KO & 32) != 0)  // timing probe: same bytes, fully coalesced (wrong data)
-        src = (const void*)(x + ((size_t)(blk & 4095) * 8 + (k & 7)) * 2048 + (size_t)((wid + 4 * j) * 64 + lane) * 4);
       // every wave issues DPW DMAs (wave-uniform vmcnt counts); those past NINSTR go to the sink
       dma16(src, wid + 4 * j < G::NINSTR ? raw + stage * Q_RAW + (wid + 4 * j) * 1024 : sink);
     }
@@ -113,23 +110,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // U: lane (co = l16, q) of wave (e row) wid, n tile nt: 8 floats U[chunk][wid][co][q][j][s]
   const float* ub = U + (((size_t)wid * CO + n0 + l16) * 4 + q) * 8;
   auto load_u = [&](int k, f32x4 (&u)[3][2]) __attribute__((always_inline)) {
-    if constexpr (KO & 4) {
-#pragma unroll
-      for (int nt = 0; nt < 3; ++nt) u[nt][0] = u[nt][1] = f32x4{1.f, 1.f, 1.f, 1.f} * (float)k;
-      return;
-    }
-    if constexpr (KO & 128) {  // timing probe: lane-varying operands without loads
-#pragma unroll
-      for (int nt = 0; nt < 3; ++nt)
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-            u[nt][h][c] = (float)(((unsigned)lane * 2654435761u + (unsigned)k * 40503u + nt * 97 + h * 13 + c) & 0xffffu) * 1e-4f;
-      return;
-    }
-    // KO & 64: every chunk re-reads chunk 0's operands (L1-resident, same values) -- timing probe
-    const float* b = (KO & 64) ? ub : ub + (size_t)(k < nchunk ? k : 0) * 4 * CO * 32;
+    const float* b = ub + (size_t)(k < nchunk ? k : 0) * 4 * CO * 32;
 #pragma unroll
     for (int nt = 0; nt < 3; ++nt)
 #pragma unroll
@@ -140,11 +121,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int raw_off = (tt / (PT * PT)) * G::PIX * 8 + (2 * ((tt / PT) % PT) * G::SIDE + 2 * (tt % PT)) * 8 + cc;
   const int v_off = (((tt & 15) * 4 + (cc >> 1)) * 2 + (tt >> 4)) * 2 + (cc & 1);  // V[e][tile&15][ci>>1][pp][ci&1]
   auto transform_read = [&](int rstage, float (&d)[16]) __attribute__((always_inline)) {
-    if constexpr (KO & 1) {
-#pragma unroll
-      for (int i2 = 0; i2 < 16; ++i2) d[i2] = (float)(rstage + i2);
-      return;
-    }
     const float* rb = reinterpret_cast<const float*>(raw + rstage * Q_RAW) + raw_off;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -152,7 +128,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int c = 0; c < 4; ++c) d[4 * r + c] = rb[(r * G::SIDE + c) * 8];
   };
   auto transform_write = [&](const float (&d)[16], int vstage) __attribute__((always_inline)) {
-    if constexpr (KO & 1) return;
     float t[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -234,7 +209,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // vmcnt(DPW + 6): raw(k+2), U(k) landed; lgkmcnt(0): own V stores and operand reads done
     __builtin_amdgcn_s_waitcnt(0x0070 | (DPW + 6));
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr ((KO & 256) == 0) __builtin_amdgcn_s_barrier();  // KO 256: timing probe only
+    __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     // raw(k+4) LDS-DMAs before this chunk's LDS reads: issued after them, the compiler drains the
     // reads (lgkmcnt(0)) in front of the DMA, which stalls the wave's MFMA stream
@@ -252,36 +227,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int nt = 0; nt < 3; ++nt) {
-            if constexpr (KO & 16)
-              acc[j][m][nt][0] += ac[j][2 * m + s2] * uc[nt][j >> 1][(j & 1) * 2 + s2];
-            else
-              acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[j][2 * m + s2], uc[nt][j >> 1][(j & 1) * 2 + s2],
-                                                                   acc[j][m][nt], 0, 0, 0);
+            acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[j][2 * m + s2], uc[nt][j >> 1][(j & 1) * 2 + s2],
+                                                                 acc[j][m][nt], 0, 0, 0);
           }
     transform_write(d, (k + 2) % 3);
-    if constexpr (KO == 0) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // DS read (8 transform, 4 operand)
-      }
-#pragma unroll
-      for (int g = 0; g < DPW + 6; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (DPW LDS-DMAs, 6 U loads)
-      }
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
-      }
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // DS read (8 transform, 4 operand)
     }
+#pragma unroll
+    for (int g = 0; g < DPW + 6; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (DPW LDS-DMAs, 6 U loads)
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
   };
   if constexpr (NCH > 0) {
 #pragma unroll
@@ -298,17 +268,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // drain past-the-end fetches before LDS is reused
 
-  if constexpr ((KO & 8) != 0) {
-    float sink = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int nt = 0; nt < 3; ++nt) sink += acc[j][m][nt][0] + acc[j][m][nt][3];
-    if (sink == 1.2345f) reinterpret_cast<float*>(p.y)[tid] = sink;
-    return;
-  }
   // epilogue: unit = (tile, 4 channels); Z[i][tile][co] f32x2 (48 KB) through LDS
   constexpr int CQ = 12, UNITS = Q_BT * CQ, UPT = (UNITS + 255) / 256;
   const float* res = reinterpret_cast<const float*>(p.res);
@@ -377,12 +336,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-template <int NCH, int KO = 0, int PT = 4>
+template <int NCH, int PT = 4>
 hipError_t launch_q(const ConvParams& p, hipStream_t s) {
   constexpr int PPB = QPatch<PT>::PPB;
   const int n_patches = p.N * p.To * (p.Ho / (2 * PT)) * (p.Wo / (2 * PT));
   const int n_co = p.Cout / 48;
-  hipLaunchKernelGGL((conv_wino_q<NCH, KO, PT>), dim3(((n_patches + PPB - 1) / PPB) * n_co), dim3(256), 0, s, p, n_co,
+  hipLaunchKernelGGL((conv_wino_q<NCH, PT>), dim3(((n_patches + PPB - 1) / PPB) * n_co), dim3(256), 0, s, p, n_co,
                      n_patches);
   return hipGetLastError();
 }
@@ -401,56 +360,22 @@ hipError_t launch_winoq(const ConvParams& p, hipStream_t s) {
   if (!winoq_supported(p)) return hipErrorInvalidValue;
   if (p.Ho % 8 == 0 && p.Wo % 8 == 0) {  // 8x8-pixel patches
     switch (p.Cin >> 3) {
-      case 8: return launch_q<8, 0, 4>(p, s);
-      case 16: return launch_q<16, 0, 4>(p, s);
-      default: return launch_q<0, 0, 4>(p, s);
+      case 8: return launch_q<8, 4>(p, s);
+      case 16: return launch_q<16, 4>(p, s);
+      default: return launch_q<0, 4>(p, s);
     }
   }
   switch (p.Cin >> 3) {  // 4x4-pixel patches (28x28 maps)
-    case 8: return launch_q<8, 0, 2>(p, s);
-    case 16: return launch_q<16, 0, 2>(p, s);
-    default: return launch_q<0, 0, 2>(p, s);
+    case 8: return launch_q<8, 2>(p, s);
+    case 16: return launch_q<16, 2>(p, s);
+    default: return launch_q<0, 2>(p, s);
   }
 }
 
 #ifdef CLASFV_KNOCKOUTS
-// occupancy probe: the same kernel at one block per CU (80 KB of extra dynamic LDS)
-template <int KO>
-static hipError_t launch_q1(const ConvParams& p, hipStream_t s) {
-  const int n_patches = p.N * p.To * (p.Ho >> 3) * (p.Wo >> 3);
-  const int n_co = p.Cout / 48;
-  hipError_t e = hipFuncSetAttribute((const void*)conv_wino_q<8, KO, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     80 * 1024);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((conv_wino_q<8, KO, 4>), dim3(((n_patches + 1) / 2) * n_co), dim3(256), 80 * 1024, s, p, n_co,
-                     n_patches);
-  return hipGetLastError();
-}
-
+// tools/convbench.hip: the product dispatch
 hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko) {
-  if (ko == 0) return launch_winoq(p, s);
-  if (p.Cin != 64 || p.Ho % 8 || p.Wo % 8) return hipErrorInvalidValue;
-  switch (ko) {
-    case 0: return launch_q<8, 0>(p, s);
-    case 1: return launch_q<8, 1>(p, s);
-    case 2: return launch_q<8, 2>(p, s);
-    case 4: return launch_q<8, 4>(p, s);
-    case 6: return launch_q<8, 6>(p, s);
-    case 8: return launch_q<8, 8>(p, s);
-    case 15: return launch_q<8, 15>(p, s);
-    case 16: return launch_q<8, 16>(p, s);
-    case 24: return launch_q<8, 24>(p, s);
-    case 32: return launch_q<8, 32>(p, s);
-    case 64: return launch_q<8, 64>(p, s);
-    case 128: return launch_q<8, 128>(p, s);
-    case 512: return launch_q1<0>(p, s);
-    case 513: return launch_q1<1>(p, s);
-    case 514: return launch_q1<2>(p, s);
-    case 520: return launch_q1<8>(p, s);
-    case 768: return launch_q1<256>(p, s);
-    case 256: return launch_q<8, 256>(p, s);
-  }
-  return hipErrorInvalidValue;
+  (void)ko;
+  return launch_winoq(p, s);
 }
-
 #endif

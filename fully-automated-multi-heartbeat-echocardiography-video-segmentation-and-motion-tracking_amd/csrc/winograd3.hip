@@ -50,8 +50,7 @@ static_assert(R_Z <= R_LDS, "epilogue exchange");
 
 __device__ inline int rpos(int col) { return col + (col >> 2); }
 
-// KO != 0 only in tools/convbench.hip timing probes: 64 = every chunk re-reads chunk 0's U (L1).
-template <int NCH, int KO = 0>
+template <int NCH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino_r(ConvParams p, int n_co,
                                                                                              int n_patches) {
   __shared__ __align__(16) char smem[R_LDS];
@@ -98,7 +97,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // U: lane (co = l16, q) of wave (H row) i, n tile nt: 12 floats U[chunk][i][co][q][j][s]
   const float* ub = U + (((size_t)wid * CO + n0 + l16) * 4 + q) * 12;
   auto load_u = [&](int k, f32x4 (&u)[3][3]) __attribute__((always_inline)) {
-    const float* b = (KO & 64) ? ub : ub + (size_t)(k < nchunk ? k : 0) * 4 * CO * 48;
+    const float* b = ub + (size_t)(k < nchunk ? k : 0) * 4 * CO * 48;
 #pragma unroll
     for (int nt = 0; nt < 3; ++nt)
 #pragma unroll
@@ -343,11 +342,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-template <int NCH, int KO = 0>
+template <int NCH>
 hipError_t launch_r(const ConvParams& p, hipStream_t s) {
   const int n_patches = p.N * p.To * (p.Ho >> 3) * (p.Wo >> 3);
   const int n_co = p.Cout / 48;
-  hipLaunchKernelGGL((conv_wino_r<NCH, KO>), dim3(((n_patches + 1) / 2) * n_co), dim3(256), 0, s, p, n_co, n_patches);
+  hipLaunchKernelGGL((conv_wino_r<NCH>), dim3(((n_patches + 1) / 2) * n_co), dim3(256), 0, s, p, n_co, n_patches);
   return hipGetLastError();
 }
 
@@ -366,13 +365,10 @@ hipError_t launch_winor(const ConvParams& p, hipStream_t s) {
 }
 
 #ifdef CLASFV_KNOCKOUTS
+// tools/convbench.hip: the product dispatch
 hipError_t launch_winor_ko(const ConvParams& p, hipStream_t s, int ko) {
-  if (p.Cin != 64) return hipErrorInvalidValue;
-  switch (ko) {
-    case 0: return launch_r<8, 0>(p, s);
-    case 64: return launch_r<8, 64>(p, s);
-  }
-  return hipErrorInvalidValue;
+  (void)ko;
+  return launch_winor(p, s);
 }
 #endif
 

@@ -3,7 +3,7 @@
 # (FETCH_SIZE and WRITE_SIZE each in a pass of its own), fp32 and bf16 headline runs.
 # usage: bash tools/gpu_profile.sh OUTDIR
 out=${1:-gpurun_out/prof}; mkdir -p $out; export TMPDIR=/tmp
-B="bench.py --steps 2 --warmup 1 --cpu-baseline 0 --extra-bf16 0"
+B="bench.py --steps 2 --warmup 1 --cpu-baseline 0 --extra-bf16 0 --extra-c3 0"
 for dt in fp32 bf16; do
   mkdir -p $out/$dt
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f rocpd csv -T -d $out/$dt/trace -o t -- python3 $B --dtype $dt > $out/$dt/trace.log 2>&1 || { echo "trace $dt failed"; tail -20 $out/$dt/trace.log; exit 1; }
