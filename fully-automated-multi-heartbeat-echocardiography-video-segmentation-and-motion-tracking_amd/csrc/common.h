@@ -24,7 +24,6 @@ struct ConvParams {
   int Cin2;
   int stem;           // fp32 4-channel input (3 + pad): register-staged kernel, per-float4 tap decode
   int in_bf16, out_bf16;
-  const void* w_alt;  // second weight image of the same conv for another kernel (conv_winot3's U layout)
 };
 
 // Decoder tap: low-resolution projection P_i = (s1 * W_i) . f_i, channels-last with 64 channels.
@@ -68,8 +67,6 @@ bool winot_supported(const ConvParams& p);
 hipError_t launch_winot(const ConvParams& p, hipStream_t s);
 // U[cin_p/8][6][cout_p/64][64][8] from folded weights w[cout][cin][3] (double).
 void winot_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
-// The same values in conv_winot3's layout U3[cin_p/8][3][cout_p][4][2][2] (p.w_alt).
-void winot3_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 // Patch-staged bf16 implicit GEMM for stride-1 1x3x3 convs (conv_patch.hip); p.w = conv_dma's image.
 bool patch_bf16_supported(const ConvParams& p);
 hipError_t launch_patch_bf16(const ConvParams& p, hipStream_t s);

@@ -80,7 +80,6 @@ struct Conv {
   float* dwino = nullptr;  // Winograd F(2x2,3x3) transformed weights (fp32 stride-1 1x3x3 convs)
   float* dwinor = nullptr;  // Winograd F(2x4,3x3) transformed weights (the same convs, Cin <= 128)
   float* dwinot = nullptr;  // Winograd F(4,3)-in-time transformed weights (fp32 stride-1 3x1x1 convs)
-  float* dwinot3 = nullptr;  // the same values in conv_winot3's layout
 };
 
 // fp32 stride-1 1x3x3 convs run on the fused Winograd kernel unless CLASFV_WINOGRAD=0.
@@ -360,7 +359,6 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   }
   if (c.dwinot) {
     p.w = c.dwinot;
-    p.w_alt = c.dwinot3;
     if (winot_supported(p)) {
       HIP_TRY(launch_winot(p, s));
       *kname = "conv_winot";
@@ -486,7 +484,6 @@ int clasfv_destroy(clasfv_t h) {
     (void)hipFree(c.dwino);
     (void)hipFree(c.dwinor);
     (void)hipFree(c.dwinot);
-    (void)hipFree(c.dwinot3);
   }
   for (auto& c : h->proj) (void)hipFree(c.dw);
   (void)hipFree(h->b1);
@@ -548,9 +545,8 @@ int clasfv_finalize(clasfv_t h) {
     (void)hipFree(c.dwino);
     (void)hipFree(c.dwinor);
     (void)hipFree(c.dwinot);
-    (void)hipFree(c.dwinot3);
     c.dw = c.db = nullptr;
-    c.dwino = c.dwinor = c.dwinot = c.dwinot3 = nullptr;
+    c.dwino = c.dwinor = c.dwinot = nullptr;
     bn_scale_shift(h, c.bn, c.cout, s, t);
     const auto& w = P(h, c.w + ".weight");
     const int taps = c.kt * c.kh * c.kw;
@@ -578,8 +574,6 @@ int clasfv_finalize(clasfv_t h) {
       std::vector<float> u((size_t)6 * c.cin_p * c.cout_p);
       winot_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, u.data());
       if ((rc = upload(u, &c.dwinot))) return rc;
-      winot3_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, u.data());
-      if ((rc = upload(u, &c.dwinot3))) return rc;
     }
   }
   // comb_1 + BN1 folded, split per tap (concat order stem, layer1, layer2, layer3, layer4)

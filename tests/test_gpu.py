@@ -502,17 +502,17 @@ def test_winograd_path_matches_direct_conv(model, monkeypatch, shape):
 
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112)])
 def test_kernel_variants_bitexact(model, monkeypatch, shape):
-    """The patch-tiled spatial Winograd kernel (conv_wino_q) and the 12-wave temporal one
-    (conv_winot2) compute the same products in the same accumulation order as conv_wino / conv_winot:
+    """The patch-tiled spatial Winograd kernel (conv_wino_q) and the rolling-halo temporal one
+    (conv_winot5) compute the same products in the same accumulation order as conv_wino / conv_winot:
     the forward must be bit-identical with them switched off."""
     rng = np.random.default_rng(23)
     x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
     s_new, m_new = model(x)
     monkeypatch.setenv("CLASFV_NO_WINO_PATCH", "1")
-    monkeypatch.setenv("CLASFV_NO_WINOT2", "1")
+    monkeypatch.setenv("CLASFV_WINOT_REFERENCE", "1")
     s_old, m_old = model(x)
     monkeypatch.delenv("CLASFV_NO_WINO_PATCH")
-    monkeypatch.delenv("CLASFV_NO_WINOT2")
+    monkeypatch.delenv("CLASFV_WINOT_REFERENCE")
     assert torch.equal(s_new, s_old) and torch.equal(m_new, m_old)
 
 

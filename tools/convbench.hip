@@ -105,20 +105,6 @@ int main(int argc, char** argv) {
   p.x = bf ? to_bf16_dev(nx, 0.f, 1.f, 1) : dev_random(nx, 0.f, 1.f, 1);
   const size_t nw = winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
   p.w = bf ? to_bf16_dev(nw, -0.05f, 0.05f, 2) : dev_random(nw, -0.05f, 0.05f, 2);
-  if (winot) {  // conv_winot3's layout of the same U values (winot3_transform_weights)
-    std::vector<float> hu(nw), hu3(nw);
-    CK(hipMemcpy(hu.data(), p.w, nw * 4, hipMemcpyDeviceToHost));
-    for (int k = 0; k < Cin / 8; ++k)
-      for (int e = 0; e < 6; ++e)
-        for (int o = 0; o < Cout; ++o)
-          for (int c8 = 0; c8 < 8; ++c8)
-            hu3[(((((size_t)k * 3 + e / 2) * Cout + o) * 4 + c8 / 2) * 2 + e % 2) * 2 + c8 % 2] =
-                hu[(((size_t)k * 6 + e) * Cout + o) * 8 + c8];
-    void* d;
-    CK(hipMalloc(&d, nw * 4));
-    CK(hipMemcpy(d, hu3.data(), nw * 4, hipMemcpyHostToDevice));
-    p.w_alt = d;
-  }
   p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
   p.res = getenv("CB_NORES") ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
   CK(hipMalloc(&p.y, ny * 4));
