@@ -18,6 +18,9 @@ Also reported on the same line (rank 0):
                 reference's -d cpu loop runs them (src/fuse_utils.py:53-61), plus one video's plumbing
   bf16          BASELINE config[4]: the same workload with the bf16 encoder
   config3       BASELINE config[3]: 64-frame 224x224 clips through the model forward
+  stream        the same per-video work fed from HOST uint8 frames through the pipelined front end
+                (pinned H2D overlapped with compute, device preprocessing, async D2H of the masks):
+                the PCIe-inclusive rate, never the headline value
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 via torch.distributed.run.
 """
@@ -61,6 +64,8 @@ def parse():
     ap.add_argument("--extra-c3", type=int, default=1,
                     help="also time BASELINE config[3] (64x224x224 clips, model forward); reported as 'config3'")
     ap.add_argument("--c3-batch", type=int, default=8, help="64x224x224 clips per forward in the config3 run")
+    ap.add_argument("--extra-stream", type=int, default=1,
+                    help="also time the pipelined front end on host uint8 videos (PCIe-inclusive); reported as 'stream'")
     ap.add_argument("--workload", default="c1", choices=["c1", "c3"],
                     help="c1: config[1] fused video pipeline (headline); c3: only the config[3] forward")
     return ap.parse_args()
@@ -237,7 +242,7 @@ def main():
         return {"value": round(n / dt, 3), "unit": "64x224x224 clips/s", "ms_per_step": round(dt / steps * 1e3, 3),
                 "clips_per_step": args.c3_batch * world, "forward": forward_stats(kt, args.c3_batch * steps,
                                                                                  GFLOP_PER_CLIP_C3, peak),
-                "roofline": kernel_roofline(kt, peak, model.engine.dtype),
+                "roofline": kernel_roofline(kt, peak, model.engine.dtype + "_c3"),  # no c3 PMC profile: traffic null
                 "note": "BASELINE config[3]: (N,3,64,224,224) model forward (seg + motion), the reference's "
                         "forward signature; the CLI path is fixed at 112x112 (src/fuse_utils.py:22)"}
 
@@ -293,6 +298,23 @@ def main():
 
     c3 = c3_run(max(2, args.steps // 2), 1) if args.extra_c3 else None
 
+    stream = None
+    if args.extra_stream and world == 1:
+        from clasfv_amd.stream import VideoStream
+        hv = [S.echo_video_uint8(args.frames, seed=v) for v in range(8)]
+        vs = VideoStream(model, num_clips=args.fuse, step=args.step, fuse_method=args.fuse_method,
+                         batch_size=args.batch_size)
+        vs.run(hv[:2])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        vs.run(hv)
+        dts = time.perf_counter() - t0
+        stream = {"value": round(n_total * len(hv) / dts, 3), "unit": "clips/s", "videos": len(hv),
+                  "ms_per_video": round(dts / len(hv) * 1e3, 3),
+                  "note": "host (T,112,112,3) uint8 frames -> pinned H2D on a copy stream overlapped with the "
+                          "previous video's compute -> device resize/normalise -> clips -> forward -> fusion -> "
+                          "async D2H of the uint8 masks; PCIe-inclusive, one host sync per batch of videos"}
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         cpu = cpu_baseline(args, S)
@@ -329,6 +351,7 @@ def main():
             "parity": parity,
             "bf16": bf16,
             "config3": c3,
+            "stream": stream,
             "lv_fraction": round(lv_frac, 4),
         }
         print(json.dumps(line), flush=True)

@@ -260,22 +260,23 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) vo
 // Each lane transforms its own (tile column, channel pair) from the raw frames into MFMA B operands
 // (no V round trip through LDS). A wave owns 2 tiles (adjacent in time: they share 2 of their 10
 // frames) x 64 channels: 96 MFMAs per chunk and barrier; 2 LDS stages, 2 blocks per CU.
-template <int TS>
+template <int TS, int NT>
 struct T5 {
   static constexpr int P = 16 * 8 / TS;          // columns per block
   static constexpr int NF = 4 * TS + 2;          // raw frames per chunk
   static constexpr int RAW_I = NF * P * 2 / 64;  // raw DMA wave-instructions per chunk
-  static constexpr int U_I = 12;                 // U: 6 e x 64 co x 32 B
+  static constexpr int CB = 16 * NT;             // output channels per block (and per wave)
+  static constexpr int U_I = 6 * CB * 32 / 1024; // U: 6 e x CB co x 32 B
   static constexpr int NI = RAW_I + U_I;
   static constexpr int STAGE = NI * 1024;
   static constexpr int LDS = 2 * STAGE;
   static_assert(NF * P * 2 % 64 == 0, "whole DMA instructions");
 };
 
-template <int TS>
+template <int TS, int NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_winot5(ConvParams p, int n_co,
                                                                                              int n_seg, int n_cols) {
-  using G = T5<TS>;
+  using G = T5<TS, NT>;
   extern __shared__ __align__(16) char smem[];
   const float* x = reinterpret_cast<const float*>(p.x);
   const float* U = reinterpret_cast<const float*>(p.w);
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int blk = xcd_swizzle_t(blockIdx.x, gridDim.x);
   const int co_blk = blk % n_co, rest = blk / n_co;
   const int seg = rest % n_seg, cb = rest / n_seg;
-  const int col0 = cb * G::P, co0 = co_blk * 64;
+  const int col0 = cb * G::P, co0 = co_blk * G::CB;
   const int T = p.To, HW = p.Ho * p.Wo, C = p.Cin, CO = p.Cout;
   const int t_seg = seg * 4 * TS;
   const int nchunk = C >> 3;
@@ -310,8 +311,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const int n = gc / HW, pix = gc - n * HW;
       off = (unsigned)(((n * T + t) * HW + pix) * C + half * 4) * 4u;
     } else if (I < G::NI) {
-      const int s = (I - G::RAW_I) * 64 + lane;  // 0 .. 767: (e, co, stored half)
-      const int e = s >> 7, co = (s >> 1) & 63, half = (s & 1) ^ ((co >> 3) & 1);
+      const int s = (I - G::RAW_I) * 64 + lane;  // (e, co, stored half)
+      const int e = s / (2 * G::CB), co = (s >> 1) % G::CB, half = (s & 1) ^ ((co >> 3) & 1);
       off = (unsigned)((e * CO + co0 + co) * 8 + half * 4) * 4u;
     }
     d_off[j] = off;
@@ -338,13 +339,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int t0w = t_seg + 4 * (j0 % TS);
   const bool pad_lo = t0w == 0, pad_hi = t0w + 8 >= T;
 
-  f32x4 acc[6][2][4];
+  f32x4 acc[6][2][NT];
 #pragma unroll
   for (int e = 0; e < 6; ++e)
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[e][m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int nt = 0; nt < NT; ++nt) acc[e][m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   issue(0, 0);
   __builtin_amdgcn_sched_barrier(0);
@@ -378,15 +379,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
-      f32x2 u[4];
+      f32x2 u[NT];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) u[nt] = *reinterpret_cast<const f32x2*>(st + u_rd + (e * 64 + nt * 16) * 8);
+      for (int nt = 0; nt < NT; ++nt) u[nt] = *reinterpret_cast<const f32x2*>(st + u_rd + (e * G::CB + nt * 16) * 8);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
+          for (int nt = 0; nt < NT; ++nt)
             acc[e][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[nt][s2], v[m][e][s2], acc[e][m][nt], 0, 0, 0);
     }
   }
@@ -403,7 +404,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   for (int m = 0; m < 2; ++m) {
     const int t0 = t0w + 4 * m;
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
+    for (int nt = 0; nt < NT; ++nt) {
       const int co = co0 + 16 * nt + 4 * q;
       const size_t o = ((size_t)(n * T + t0) * HW + pix) * CO + co;
       const f32x4 bv = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -434,27 +435,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-template <int TS>
+template <int TS, int NT>
 hipError_t winot5_launch(const ConvParams& p, hipStream_t s) {
-  using G = T5<TS>;
+  using G = T5<TS, NT>;
   static bool attr = false;
   if (!attr && G::LDS > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_winot5<TS>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    hipError_t e = hipFuncSetAttribute((const void*)conv_winot5<TS, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       G::LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const int n_cols = p.N * p.Hi * p.Wi;
   const int n_seg = (p.Ti / 4) / TS;
-  const int n_co = p.Cout / 64;
+  const int n_co = p.Cout / G::CB;
   const int nb = ((n_cols + G::P - 1) / G::P) * n_seg * n_co;
-  hipLaunchKernelGGL((conv_winot5<TS>), dim3(nb), dim3(256), G::LDS, s, p, n_co, n_seg, n_cols);
+  hipLaunchKernelGGL((conv_winot5<TS, NT>), dim3(nb), dim3(256), G::LDS, s, p, n_co, n_seg, n_cols);
   return hipGetLastError();
 }
 
-hipError_t winot5_dispatch(const ConvParams& p, hipStream_t s) {
+// 64 channels per wave (NT = 4); 32 when that leaves fewer than two blocks per CU (layer3 maps).
+hipError_t winot5_dispatch(const ConvParams& p, hipStream_t s, int force_nt = 0) {
   const int tt = p.Ti / 4;
-  if (tt % 4 == 0) return winot5_launch<4>(p, s);
-  return winot5_launch<2>(p, s);  // T = 8
+  const int ts = tt % 4 == 0 ? 4 : 2;
+  const long blocks64 = (long)((p.N * p.Hi * p.Wi + 16 * 8 / ts - 1) / (16 * 8 / ts)) * (tt / ts) * (p.Cout / 64);
+  const int nt = force_nt ? force_nt : (blocks64 >= 512 ? 4 : 2);
+  if (ts == 4) return nt == 4 ? winot5_launch<4, 4>(p, s) : winot5_launch<4, 2>(p, s);
+  return nt == 4 ? winot5_launch<2, 4>(p, s) : winot5_launch<2, 2>(p, s);
 }
 
 }  // namespace
@@ -501,6 +507,8 @@ hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko) {
       return hipGetLastError();
     }
     case 500: return winot5_dispatch(p, s);
+    case 502: return winot5_dispatch(p, s, 2);
+    case 504: return winot5_dispatch(p, s, 4);
   }
   return hipErrorInvalidValue;
 }

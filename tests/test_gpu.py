@@ -687,3 +687,19 @@ def test_normalizer_workspace_per_call_streams():
         xb = zeroone_normalize_(b.clone())
     torch.cuda.synchronize()
     assert torch.equal(xa, ra) and torch.equal(xb, rb)
+
+
+def test_video_stream_matches_per_video_pipeline(model):
+    """Pipelined multi-video front end (pinned H2D on a copy stream, device preprocessing, no host
+    sync between videos) == the drop-in per-video path on the same frames."""
+    import clasfv_amd.synthetic as S
+    from clasfv_amd import fuse_utils as FU
+    from clasfv_amd.preprocess import preprocess_video
+    from clasfv_amd.stream import VideoStream
+    vids = [S.echo_video_uint8(T, seed=40 + T) for T in (70, 100, 45, 64)]
+    vids.append(S.echo_video_uint8(50, 96, 128, seed=7))  # resized to 112x112 on the device
+    got = VideoStream(model, num_clips=3, fuse_method="simple").run(vids)
+    for v, g in zip(vids, got):
+        ref = FU.segment_a_video_with_fusion(preprocess_video(v), model, num_clips=3, fuse_method="simple")
+        assert g.dtype == np.int64
+        np.testing.assert_array_equal(g, ref)
