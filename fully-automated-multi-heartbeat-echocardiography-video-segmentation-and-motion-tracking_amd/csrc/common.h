@@ -67,7 +67,8 @@ bool winot_supported(const ConvParams& p);
 hipError_t launch_winot(const ConvParams& p, hipStream_t s);
 // U[cin_p/8][6][cout_p/64][64][8] from folded weights w[cout][cin][3] (double).
 void winot_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
-// Patch-staged bf16 implicit GEMM for stride-1 1x3x3 convs (conv_patch.hip); p.w = conv_dma's image.
+// Patch-staged bf16 implicit GEMM for stride-1 1x3x3 and 3x1x1 convs (conv_patch.hip); p.w = conv_dma's
+// image.
 bool patch_bf16_supported(const ConvParams& p);
 hipError_t launch_patch_bf16(const ConvParams& p, hipStream_t s);
 hipError_t launch_decoder(const DecParams& p, hipStream_t s);

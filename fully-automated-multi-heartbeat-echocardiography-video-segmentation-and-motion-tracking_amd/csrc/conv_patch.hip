@@ -1,40 +1,41 @@
-// Patch-staged bf16 implicit GEMM for the stride-1 1x3x3 spatial convs of the R(2+1)D-18 encoder
-// (torchvision Conv2Plus1D spatial half, called from src/model/R2plus1D_18_MotionNet.py:29-37),
-// BASELINE config[4] (bf16 activations/weights, fp32 accumulation).
+// Patch-staged bf16 implicit GEMM for the stride-1 convs of the R(2+1)D-18 encoder in bf16
+// (BASELINE config[4]: bf16 activations/weights, fp32 accumulation): the Conv2Plus1D spatial 1x3x3
+// and temporal 3x1x1 halves (torchvision Conv2Plus1D, called from
+// src/model/R2plus1D_18_MotionNet.py:29-37) and the stem's temporal 3x1x1 conv.
 //
 // Why: conv_dma (conv.hip) gathers the im2col A tile straight from global memory, so every input
-// voxel crosses the L2 -> LDS path once per 3x3 tap; in bf16 the MFMAs are 16x faster than in fp32
-// and that gather, not the matrix cores, sets the time (layer1 64->160: 2.08 ms, 267 TF alg.).
-// Here a block's output tile is 2 frames x 8 rows x 8 columns (128 voxels); for each 32-channel
-// chunk the 2 x 10 x 10 input patch (200 voxels x 64 B) is copied to LDS ONCE and the nine taps
-// read their A fragments from it at pixel offsets kh*10 + kw: 9 x 128 gathered rows become 200.
-//  * K order: chunk-major, tap-minor (step s = 9*chunk + tap); weights keep conv_dma's image
+// voxel crosses the L2 -> LDS path once per tap; in bf16 the MFMAs are 16x faster than in fp32 and
+// that gather, not the matrix cores, sets the time. Here a block's output tile is 4 frames x 64
+// pixels (8x8 for the spatial conv, 64 consecutive pixels of the flattened map for the temporal
+// one) x 16*NT output channels; for each 32-channel chunk the input patch it needs (4 x 10 x 10 or
+// 6 x 64 pixels x 64 B) is copied to LDS once and every tap reads its A fragments from it at a
+// pixel offset: 9 x 256 (3 x 256) gathered rows become 400 (384).
+//  * wave w owns output frame t0 + w: 4 m tiles (64 voxels) x NT n tiles (up to 160 channels), so
+//    per 32-deep K step a wave issues 4*NT MFMAs (v_mfma_f32_16x16x32_bf16) on 4 + NT LDS reads,
+//    with one block barrier per step;
+//  * K order: chunk-major, tap-minor (step s = TAPS*chunk + tap); weights keep conv_dma's image
 //    [Cout_alloc][Kp] with k = tap*Cin + c, so one B row segment is w[n][tap*Cin + 32*chunk ..];
 //  * patch image: double-buffered, pixel rows of 64 B, 16-B slot q of pixel p stored at
-//    q ^ g[(p >> 2) & 3] (the tap shift makes some reads 2-way conflicted; B reads are conflict-free);
-//  * B ring: 3 stages of NT x 16 rows x 64 B, one per step, as in conv_dma; all copies are
-//    LDS-DMA (global_load_lds_dwordx4) with per-lane source addresses (zero block for halo pixels);
-//  * counted vmcnt: at step s a wave waits for its own B(s) (and, implied by in-order completion,
-//    the patch of the step's chunk), then a block barrier; the next chunk's patch is issued at the
-//    chunk's tap 0, after the barrier that retires the buffer's previous chunk;
+//    q ^ g[(p >> 2) & 3]; B ring: 3 stages of NT x 16 rows x 64 B, one per step. At NT = 10 the
+//    spatial kernel's LDS is exactly 80 KiB: two blocks (8 waves) per CU;
+//  * all copies are LDS-DMA (global_load_lds_dwordx4), 1-KiB pieces dealt round-robin to the
+//    waves (piece j to wave j % 4, no sink slots); counted vmcnt with per-wave immediates: at step
+//    s a wave waits for its own share of B(s) (and, by in-order completion, of the chunk's patch),
+//    then a block barrier; the next chunk's patch is issued at the chunk's tap 0;
 //  * epilogue: the MFMAs compute D^T = W . A^T, so a lane holds 4 consecutive output channels of
 //    one voxel: folded-BN bias, optional residual, ReLU, 8-B bf16 stores; voxels outside the map
-//    (ragged 28/14/7-pixel maps) are masked.
+//    (ragged 28/14/7-pixel maps, partial pixel tiles) are masked.
 #include <hip/hip_bf16.h>
 #include <stdlib.h>
+
+#include <utility>
 
 #include "common.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 namespace {
-
-constexpr int PT = 2, PR = 8, PC = 8;             // output tile (frames, rows, columns)
-constexpr int QR = PR + 2, QC = PC + 2;           // input patch rows / columns (3x3 halo)
-constexpr int PPIX = PT * QR * QC;                // 200 patch pixels
-constexpr int P_INS = (PPIX * 64 + 1023) / 1024;  // 13 DMA pieces of 1 KiB
-constexpr int P_PW = (P_INS + 3) / 4;             // 4 pieces per wave (tail pieces fill the pad)
-constexpr int P_BYTES = 4 * P_PW * 1024;          // 16 KiB per patch buffer
 
 // slot swizzle g = {0, 2, 3, 1} as arithmetic: a runtime-indexed constant array is a global load,
 // and its in-order vmcnt wait would drain the whole DMA ring in front of every A read
@@ -45,147 +46,211 @@ __device__ inline int xcd_swizzle_p(int b, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
-template <int NT>
-__global__ __launch_bounds__(256) void conv_patch_bf16(ConvParams p, int n_tiles, int tiles_w, int tiles_h, int tiles_t) {
-  constexpr int BN = 16 * NT, S = 3;
-  constexpr int B_PW = (NT + 3) / 4;
-  constexpr int B_STAGE = NT * 1024;
-  constexpr int B0 = 2 * P_BYTES;
-  constexpr int JUNK = B0 + S * B_STAGE;
-  __shared__ __align__(16) char smem[JUNK + 1024];
+// Patch geometry: KT = 1 -> 1x3x3 conv on 8x8-pixel tiles, KT = 3 -> 3x1x1 conv on 64 pixels;
+// FR output frames per block.
+template <int KT, int FR>
+struct PGeo {
+  static constexpr bool SPATIAL = KT == 1;
+  static constexpr int TAPS = SPATIAL ? 9 : 3;
+  static constexpr int MT = FR;                              // m tiles (16 voxels) per wave
+  static constexpr int PF = FR + KT - 1;                     // patch frames
+  static constexpr int PR = SPATIAL ? 10 : 1, PC = SPATIAL ? 10 : 64;
+  static constexpr int FPIX = PR * PC;                       // patch pixels per frame
+  static constexpr int PPIX = PF * FPIX;
+  static constexpr int PIECES = (PPIX + 15) / 16;            // 1-KiB DMA pieces (16 pixels x 64 B)
+  static constexpr int BYTES = PIECES * 1024;
+};
+
+template <int V>
+__device__ inline void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(V) : "memory");
+}
+
+// address (bytes) of one 16-B LDS-DMA source: uniform base + per-lane offset (the saddr form)
+__device__ inline void dma16(const char* base, unsigned off, void* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + off),
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+__device__ inline void dma16(const void* src, void* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+template <int... I, class F>
+__device__ inline void for_taps(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+
+// S = B ring depth (B(s) is fetched S-1 steps ahead); OCC = blocks per CU (the LDS budget and the
+// register cap follow from it).
+template <int NT, int KT, int FR, int S, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void conv_patch_bf16(
+    ConvParams p, int n_tiles, int ptw, int npt, int t_tiles) {
+  using G = PGeo<KT, FR>;
+  constexpr int TAPS = G::TAPS, MT = G::MT;
+  static_assert(S >= 3 && S <= TAPS + 1, "wait counts below assume S - 1 <= TAPS");
+  constexpr int PW = (G::PIECES + 3) / 4, BW = (NT + 3) / 4;  // DMAs per wave (uniform counts)
+  constexpr int B_STAGE = NT * 1024, B0 = 2 * G::BYTES, SINK = B0 + S * B_STAGE;
+  constexpr int LDS = SINK + 1024;
+  static_assert(OCC * LDS <= 160 * 1024, "LDS budget");
+  __shared__ __align__(16) char smem[LDS];
 
   const __bf16* x = reinterpret_cast<const __bf16*>(p.x);
-  const __bf16* w = reinterpret_cast<const __bf16*>(p.w);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int tile = xcd_swizzle_p(blockIdx.x, gridDim.x);
-  const int n0 = (tile % n_tiles) * BN;
-  tile /= n_tiles;
-  const int w0 = (tile % tiles_w) * PC;
-  tile /= tiles_w;
-  const int h0 = (tile % tiles_h) * PR;
-  tile /= tiles_h;
-  const int t0 = (tile % tiles_t) * PT;
-  const int nclip = tile / tiles_t;
   const int q = lane >> 4, l16 = lane & 15;
-
-  // patch DMA descriptors: piece j = wid + 4*i writes pixels 16j .. 16j+15, lane -> pixel
-  // 16j + lane/4, physical slot lane & 3 (fetches logical slot (lane & 3) ^ g)
-  int pv[P_PW], ps[P_PW];
-#pragma unroll
-  for (int i = 0; i < P_PW; ++i) {
-    const int pix = (wid + 4 * i) * 16 + (lane >> 2);
-    ps[i] = (lane & 3) ^ gsw((pix >> 2) & 3);
-    pv[i] = -1;
-    if (pix < PPIX) {
-      const int ptt = pix / (QR * QC), r = pix - ptt * (QR * QC);
-      const int pr = r / QC, pc = r - pr * QC;
-      const int ti = t0 + ptt, hi = h0 - 1 + pr, wi = w0 - 1 + pc;
-      if (ti < p.Ti && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi)
-        pv[i] = ((nclip * p.Ti + ti) * p.Hi + hi) * p.Wi + wi;
-    }
-  }
-  // B DMA descriptors (conv_dma's swizzled 64-B rows)
-  const int drow = lane >> 2;
-  const int dq = (lane & 3) ^ gsw((drow >> 2) & 3);
-  const __bf16* wrow[B_PW];
-#pragma unroll
-  for (int i = 0; i < B_PW; ++i) {
-    const int j = wid + 4 * i;
-    wrow[i] = w + (size_t)(n0 + (j < NT ? j : 0) * 16 + drow) * p.Kp + 8 * dq;
-  }
-
+  int tile = xcd_swizzle_p(blockIdx.x, gridDim.x);
+  const int n0 = (tile % n_tiles) * 16 * NT;
+  tile /= n_tiles;
+  const int pt = tile % npt;
+  tile /= npt;
+  const int t0 = (tile % t_tiles) * FR;
+  const int clip = tile / t_tiles;
+  const int HW = p.Hi * p.Wi;
+  const int h0 = G::SPATIAL ? (pt / ptw) * 8 : 0, w0 = G::SPATIAL ? (pt % ptw) * 8 : 0;
+  const int hw0 = G::SPATIAL ? 0 : pt * 64;
   const int Cin = p.Cin;
-  auto issue_patch = [&](int c, int buf) {
-    const int c0 = c * 32;
+
+  // patch DMA: piece j = wid + 4*i writes pixels 16j .. 16j+15, lane -> pixel 16j + lane/4,
+  // physical slot lane & 3 (fetches logical slot (lane & 3) ^ g); pieces past the patch land in
+  // the sink, pixels outside the map read the zero block
+  int pv[PW];
+  unsigned psl[PW];
 #pragma unroll
-    for (int i = 0; i < P_PW; ++i) {
-      const void* src = pv[i] >= 0 ? (const void*)(x + (size_t)(unsigned)pv[i] * Cin + c0 + 8 * ps[i]) : p.zero;
-      char* dst = smem + buf * P_BYTES + (wid + 4 * i) * 1024;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  for (int i = 0; i < PW; ++i) {
+    const int pix = (wid + 4 * i) * 16 + (lane >> 2);
+    psl[i] = (unsigned)(((lane & 3) ^ gsw((pix >> 2) & 3)) * 16);
+    pv[i] = -1;
+    if (pix < G::PPIX) {
+      const int f = pix / G::FPIX, r = pix - f * G::FPIX;
+      if constexpr (G::SPATIAL) {
+        const int pr = r / G::PC, pc = r - pr * G::PC;
+        const int ti = t0 + f, hi = h0 - 1 + pr, wi = w0 - 1 + pc;
+        if (ti < p.Ti && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi)
+          pv[i] = ((clip * p.Ti + ti) * p.Hi + hi) * p.Wi + wi;
+      } else {
+        const int ti = t0 - 1 + f, hw = hw0 + r;
+        if ((unsigned)ti < (unsigned)p.Ti && hw < HW) pv[i] = (clip * p.Ti + ti) * HW + hw;
+      }
+    }
+  }
+  auto issue_patch = [&](int c, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int j = wid + 4 * i;
+      const void* src = pv[i] >= 0 ? (const void*)(reinterpret_cast<const char*>(x + (size_t)pv[i] * Cin + 32 * c) + psl[i])
+                                   : p.zero;
+      dma16(src, smem + (j < G::PIECES ? buf * G::BYTES + j * 1024 : SINK));
     }
   };
-  auto issue_b = [&](int s, int slot) {
-    const int c = s / 9, tap = s - 9 * c;
-    const int koff = tap * Cin + 32 * c;
+  // B DMA (conv_dma's swizzled 64-B rows): piece j = wid + 4*i is n tile j; per-lane byte offsets
+  // from the block's weight rows, the step's K offset in the uniform base
+  const char* wb = reinterpret_cast<const char*>(p.w) + (size_t)n0 * p.Kp * 2;
+  unsigned boff[BW];
+  {
+    const int drow = lane >> 2, dq = (lane & 3) ^ gsw((drow >> 2) & 3);
 #pragma unroll
-    for (int i = 0; i < B_PW; ++i) {
+    for (int i = 0; i < BW; ++i) {
       const int j = wid + 4 * i;
-      const void* src = j < NT ? (const void*)(wrow[i] + koff) : p.zero;
-      char* dst = j < NT ? smem + B0 + slot * B_STAGE + j * 1024 : smem + JUNK;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      boff[i] = (unsigned)(((j < NT ? j : 0) * 16 + drow) * p.Kp + 8 * dq) * 2u;
+    }
+  }
+  const int nc = Cin / 32;
+  // B(c, tap) -> ring slot (TAPS*c + tap) % S; chunks past the end re-read chunk 0 into a slot
+  // nobody reads
+  auto issue_b = [&](int c, int tap, int slot) __attribute__((always_inline)) {
+    const char* base = wb + (size_t)(tap * Cin + 32 * (c < nc ? c : 0)) * 2;
+#pragma unroll
+    for (int i = 0; i < BW; ++i) {
+      const int j = wid + 4 * i;
+      dma16(base, boff[i], smem + (j < NT ? B0 + slot * B_STAGE + j * 1024 : SINK));
     }
   };
 
-  f32x4 acc[2][NT];
+  f32x4 acc[MT][NT];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nc = Cin / 32, nk = 9 * nc;
+  // A fragment i of this lane: block voxel m = 16*(MT*wid + i) + l16; LDS byte address of its
+  // 16-B slot q at every tap (patch buffer 0)
+  int aaddr[TAPS][MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = 16 * (MT * wid + i) + l16, f = m >> 6, px = m & 63;
+    const int base = G::SPATIAL ? (f * G::PR + (px >> 3)) * G::PC + (px & 7) : f * 64 + px;
+#pragma unroll
+    for (int tap = 0; tap < TAPS; ++tap) {
+      const int pix = base + (G::SPATIAL ? (tap / 3) * G::PC + tap % 3 : tap * 64);
+      aaddr[tap][i] = pix * 64 + ((q ^ gsw((pix >> 2) & 3)) << 4);
+    }
+  }
+  const int b_rd = B0 + l16 * 64 + (q ^ gsw(l16 >> 2)) * 16;
+
   issue_patch(0, 0);
-  issue_b(0, 0);
-  if (nk > 1) issue_b(1, 1);
-
-  // A fragment i of this lane: tile voxel m = 32*wid + 16*i + l16 -> patch pixel of tap (0,0)
-  int abase[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m = wid * 32 + i * 16 + l16;
-    abase[i] = ((m >> 6) * QR + ((m >> 3) & 7)) * QC + (m & 7);
+  for (int k = 0; k < S - 1; ++k) issue_b(k / TAPS, k % TAPS, k);
+  int slot = 0;  // ring slot of B(s) (wave-uniform)
+
+  for (int c = 0; c < nc; ++c) {
+    const bool more = c + 1 < nc;
+    const int pbuf = (c & 1) * G::BYTES;
+    for_taps(std::make_integer_sequence<int, TAPS>{}, [&](auto tc) __attribute__((always_inline)) {
+      constexpr int TAP = decltype(tc)::value;
+      // B(s) landed; in flight may stay B(s+1) .. B(s+S-2) and, at taps 1 .. S-1, the next chunk's
+      // patch (issued at tap 0 after B(s)). At tap 0 the chunk's own patch was issued TAPS steps
+      // ago, before B(s) whenever S - 1 <= TAPS.
+      if constexpr (TAP >= 1 && TAP <= S - 1) {
+        if (more) vm_wait<(S - 2) * BW + PW>();
+        else vm_wait<(S - 2) * BW>();
+      } else {
+        vm_wait<(S - 2) * BW>();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int T2 = (TAP + S - 1) % TAPS, C2 = (TAP + S - 1) / TAPS;
+      const int slot_new = slot == 0 ? S - 1 : slot - 1;  // (s + S - 1) % S
+      issue_b(c + C2, T2, slot_new);
+      if constexpr (TAP == 0) {
+        if (more) issue_patch(c + 1, (c + 1) & 1);
+      }
+      bf16x8 a[MT], b[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a[i] = *reinterpret_cast<const bf16x8*>(smem + pbuf + aaddr[TAP][i]);
+      const char* bs = smem + b_rd + slot * B_STAGE;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + j * 1024);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      slot = slot + 1 == S ? 0 : slot + 1;
+    });
   }
-  const int b_off = B0 + l16 * 64 + (q ^ gsw(l16 >> 2)) * 16;
+  vm_wait<0>();  // the past-the-end B fetches land before the block's LDS is released
 
-  for (int s = 0; s < nk; ++s) {
-    const int c = s / 9, tap = s - 9 * c;
-    if (s + 1 < nk) {
-      if (tap == 1 && c + 1 < nc)  // the previous step issued B(s+1) and then the next patch
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_PW + P_PW) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_PW) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (s + 2 < nk) issue_b(s + 2, (s + 2) % S);
-    if (tap == 0 && c + 1 < nc) issue_patch(c + 1, (c + 1) & 1);
-
-    const char* pb = smem + (c & 1) * P_BYTES;
-    const int kh = tap / 3, toff = kh * QC + (tap - 3 * kh);
-    bf16x8 a[2], b[NT];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int pix = abase[i] + toff;
-      a[i] = *reinterpret_cast<const bf16x8*>(pb + pix * 64 + ((q ^ gsw((pix >> 2) & 3)) << 4));
-    }
-    const char* st = smem + (s % S) * B_STAGE + b_off;
-#pragma unroll
-    for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(st + j * 1024);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-  }
-
-  // epilogue: accumulator acc[i][j] holds channels n0 + 16j + 4q .. +3 of tile voxel 32*wid + 16*i + l16
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  // epilogue: acc[i][j] holds channels n0 + 16j + 4q .. +3 of block voxel 16*(MT*wid + i) + l16
   const __bf16* res = reinterpret_cast<const __bf16*>(p.res);
   __bf16* y = reinterpret_cast<__bf16*>(p.y);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m = wid * 32 + i * 16 + l16;
-    const int to = t0 + (m >> 6), ho = h0 + ((m >> 3) & 7), wo = w0 + (m & 7);
-    if (!(to < p.To && ho < p.Ho && wo < p.Wo)) continue;
-    const size_t gm = (((size_t)nclip * p.To + to) * p.Ho + ho) * p.Wo + wo;
+  for (int i = 0; i < MT; ++i) {
+    const int m = 16 * (MT * wid + i) + l16, f = m >> 6, px = m & 63;
+    const int to = t0 + f;
+    size_t gm;
+    if constexpr (G::SPATIAL) {
+      const int ho = h0 + (px >> 3), wo = w0 + (px & 7);
+      if (!(to < p.To && ho < p.Ho && wo < p.Wo)) continue;
+      gm = (((size_t)clip * p.To + to) * p.Ho + ho) * p.Wo + wo;
+    } else {
+      const int hw = hw0 + px;
+      if (!(to < p.To && hw < HW)) continue;
+      gm = ((size_t)clip * p.To + to) * HW + hw;
+    }
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int n = n0 + j * 16 + 4 * q;
-      if (n >= p.Cout) continue;
       const size_t o = gm * p.Cout + n;
       f32x4 v = acc[i][j];
       if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
@@ -195,48 +260,143 @@ __global__ __launch_bounds__(256) void conv_patch_bf16(ConvParams p, int n_tiles
       }
       if (p.relu) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.f);
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
       }
       *reinterpret_cast<bf16x4*>(y + o) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
     }
   }
 }
 
-template <int NT>
-hipError_t launch_patch(const ConvParams& p, hipStream_t s) {
+template <int NT, int KT, int FR, int S>
+constexpr int patch_occ() {
+  constexpr int lds = 2 * PGeo<KT, FR>::BYTES + S * NT * 1024 + 1024;
+  constexpr int occ = 160 * 1024 / lds;
+  return occ > 4 ? 4 : occ;
+}
+
+struct PatchGrid {
+  int ptw, npt, tt;
+  long base;  // blocks per n tile
+};
+
+PatchGrid patch_grid(const ConvParams& p, int fr) {
+  PatchGrid g{};
+  if (p.KT == 1) {
+    g.ptw = (p.Wo + 7) / 8;
+    g.npt = g.ptw * ((p.Ho + 7) / 8);
+  } else {
+    g.npt = (p.Ho * p.Wo + 63) / 64;
+  }
+  g.tt = (p.To + fr - 1) / fr;
+  g.base = (long)p.N * g.tt * g.npt;
+  return g;
+}
+
+template <int NT, int KT, int FR, int S = 3>
+hipError_t launch_p(const ConvParams& p, hipStream_t s) {
+  const PatchGrid g = patch_grid(p, FR);
   const int n_tiles = p.Cout / (16 * NT);
-  const int tw = (p.Wo + PC - 1) / PC, th = (p.Ho + PR - 1) / PR, tt = (p.To + PT - 1) / PT;
-  const long blocks = (long)p.N * tt * th * tw * n_tiles;
-  hipLaunchKernelGGL((conv_patch_bf16<NT>), dim3((unsigned)blocks), dim3(256), 0, s, p, n_tiles, tw, th, tt);
+  hipLaunchKernelGGL((conv_patch_bf16<NT, KT, FR, S, patch_occ<NT, KT, FR, S>()>), dim3((unsigned)(g.base * n_tiles)),
+                     dim3(256), 0, s, p, n_tiles, g.ptw, g.npt, g.tt);
   return hipGetLastError();
+}
+
+// Output frames per block: 2 for the 1x3x3 convs (3 blocks per CU at NT <= 5), 4 for the 3x1x1
+// convs (the 6-frame patch halves the temporal halo's re-fetch against 2 frames; tools/bench_patch.sh).
+template <int KT>
+constexpr int product_fr() {
+  return KT == 1 ? 2 : 4;
+}
+
+template <int KT>
+hipError_t launch_nt(const ConvParams& p, int nt, hipStream_t s) {
+  constexpr int FR = product_fr<KT>();
+  switch (nt) {
+    case 10: return launch_p<10, KT, FR>(p, s);
+    case 9: return launch_p<9, KT, FR>(p, s);
+    case 8: return launch_p<8, KT, FR>(p, s);
+    case 6: return launch_p<6, KT, FR>(p, s);
+    case 5: return launch_p<5, KT, FR>(p, s);
+    case 4: return launch_p<4, KT, FR>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+// N tile: the widest (fewest A re-reads, most MFMAs per LDS read) that still gives two blocks per
+// CU; the narrowest legal one when none does (layer4's 7x7 maps).
+int patch_pick_nt(const ConvParams& p, int force_nt) {
+  const int n16 = p.Cout / 16;
+  const long base = patch_grid(p, p.KT == 1 ? product_fr<1>() : product_fr<3>()).base;
+  int pick = 0;
+  for (int nt : {10, 9, 8, 6, 5, 4}) {
+    if (n16 % nt) continue;
+    if (force_nt > 0) {
+      if (nt == force_nt) return nt;
+      continue;
+    }
+    pick = nt;
+    if (base * (n16 / nt) >= 512) break;
+  }
+  return pick;
 }
 
 }  // namespace
 
 bool patch_bf16_supported(const ConvParams& p) {
   if (!p.in_bf16 || !p.out_bf16 || p.stem || p.x2) return false;
-  if (p.KT != 1 || p.KH != 3 || p.KW != 3 || p.st != 1 || p.sh != 1 || p.sw != 1) return false;
-  if (p.pt != 0 || p.ph != 1 || p.pw != 1) return false;
-  if (p.Cin % 32 || p.Cout % 16 || p.Kp != 9 * p.Cin) return false;
+  if (p.st != 1 || p.sh != 1 || p.sw != 1) return false;
+  const bool spatial = p.KT == 1 && p.KH == 3 && p.KW == 3 && p.pt == 0 && p.ph == 1 && p.pw == 1;
+  const bool temporal = p.KT == 3 && p.KH == 1 && p.KW == 1 && p.pt == 1 && p.ph == 0 && p.pw == 0;
+  if (!spatial && !temporal) return false;
+  if (p.Cin % 32 || p.Cout % 16 || p.Kp != p.KT * p.KH * p.KW * p.Cin) return false;
   if (p.To != p.Ti || p.Ho != p.Hi || p.Wo != p.Wi) return false;
+  if (patch_pick_nt(p, 0) == 0) return false;
   // voxel indices are int32 in the kernel
   if ((long)p.N * p.Ti * p.Hi * p.Wi >= (1L << 31) / 2) return false;
   return true;
 }
 
 hipError_t launch_patch_bf16(const ConvParams& p, hipStream_t s) {
-  const int n16 = p.Cout / 16;
+  if (!patch_bf16_supported(p)) return hipErrorInvalidValue;
   static const int force_nt = getenv("CLASFV_PATCH_NT") ? atoi(getenv("CLASFV_PATCH_NT")) : 0;  // A/B
-  for (int nt : {10, 9, 8, 6, 5, 4}) {
-    if (n16 % nt || (force_nt > 0 && nt != force_nt) || (force_nt <= 0 && nt == 10)) continue;
-    switch (nt) {
-      case 10: return launch_patch<10>(p, s);
-      case 9: return launch_patch<9>(p, s);
-      case 8: return launch_patch<8>(p, s);
-      case 6: return launch_patch<6>(p, s);
-      case 5: return launch_patch<5>(p, s);
-      case 4: return launch_patch<4>(p, s);
-    }
+  const int nt = patch_pick_nt(p, force_nt);
+  return p.KT == 1 ? launch_nt<1>(p, nt, s) : launch_nt<3>(p, nt, s);
+}
+
+
+#ifdef CLASFV_KNOCKOUTS
+// tools/convbench.hip variant sweep: ko = FR*1000 + S*100 + NT (e.g. 2305 = 2 frames per block,
+// 3 ring stages, NT 5)
+namespace {
+template <int KT, int FR, int S>
+hipError_t ko_nt(const ConvParams& p, int nt, hipStream_t s) {
+  switch (nt) {
+    case 10: if constexpr (patch_occ<10, KT, FR, S>() >= 1) return launch_p<10, KT, FR, S>(p, s); break;
+    case 5: return launch_p<5, KT, FR, S>(p, s);
+    case 4: return launch_p<4, KT, FR, S>(p, s);
   }
   return hipErrorInvalidValue;
 }
+template <int KT, int FR>
+hipError_t ko_s(const ConvParams& p, int st, int nt, hipStream_t s) {
+  switch (st) {
+    case 3: return ko_nt<KT, FR, 3>(p, nt, s);
+    case 4: return ko_nt<KT, FR, 4>(p, nt, s);
+  }
+  if constexpr (KT == 1) {
+    if (st == 5) return ko_nt<KT, FR, 5>(p, nt, s);
+    if (st == 6) return ko_nt<KT, FR, 6>(p, nt, s);
+  }
+  return hipErrorInvalidValue;
+}
+}  // namespace
+
+hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko) {
+  if (ko == 0) return launch_patch_bf16(p, s);
+  const int fr = ko / 1000, st = ko / 100 % 10, nt = ko % 100;
+  if (p.Cout % (16 * nt)) return hipErrorInvalidValue;
+  if (fr == 2) return p.KT == 1 ? ko_s<1, 2>(p, st, nt, s) : ko_s<3, 2>(p, st, nt, s);
+  if (fr == 4) return p.KT == 1 ? ko_s<1, 4>(p, st, nt, s) : ko_s<3, 4>(p, st, nt, s);
+  return hipErrorInvalidValue;
+}
+#endif

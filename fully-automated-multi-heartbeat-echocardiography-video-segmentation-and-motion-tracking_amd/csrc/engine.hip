@@ -303,9 +303,14 @@ double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
     return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 1) / 2) * 16.0 * cc * 1e-9;
   if (!strcmp(kname, "conv_wino_r")) return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 3) / 4) * 24.0 * cc * 1e-9;
   if (!strcmp(kname, "conv_winot")) return 2.0 * out.n * (out.t / 4) * (double)out.h * out.w * 6.0 * cc * 1e-9;
+  if (!strcmp(kname, "conv_patch_bf16")) {  // frames x 64-pixel tiles: 2 x 8x8 for 1x3x3, 4 x 64 flat for 3x1x1
+    const int fr = c.kt == 1 ? 2 : 4;
+    const double px = c.kt == 1 ? (double)((out.h + 7) / 8 * 8) * ((out.w + 7) / 8 * 8)
+                                : (double)((out.h * out.w + 63) / 64 * 64);
+    return 2.0 * out.n * ((out.t + fr - 1) / fr * fr) * px * c.cout_p * (double)c.Kp * 1e-9;
+  }
   const double m = (double)out.n * out.t * out.h * out.w;
-  const double bm = !strcmp(kname, "conv_patch") ? 1.0 : 128.0;
-  return 2.0 * (ceil(m / bm) * bm) * c.cout_p * (double)c.Kp * 1e-9;
+  return 2.0 * (ceil(m / 128.0) * 128.0) * c.cout_p * (double)c.Kp * 1e-9;
 }
 
 int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
@@ -369,7 +374,7 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   const bool no_patch_bf16 = getenv("CLASFV_NO_PATCH_BF16") != nullptr;  // A/B switch (tests)
   if (!no_patch_bf16 && patch_bf16_supported(p)) {
     HIP_TRY(launch_patch_bf16(p, s));
-    *kname = "conv_patch";
+    *kname = "conv_patch_bf16";
     return CLASFV_OK;
   }
   int mt = 2, bn = c.cout_p;  // stem: one N tile (48 fp32 / 64 bf16 channels)

@@ -448,8 +448,8 @@ def test_forward_bf16_vs_reference_golden_config4_tolerance(model):
 
 @pytest.mark.parametrize("shape", [(1, 3, 32, 112, 112), (2, 3, 16, 64, 48)])
 def test_bf16_patch_conv_matches_direct_conv(model, monkeypatch, shape):
-    """bf16 stride-1 1x3x3 convs: the patch-staged kernel (conv_patch.hip, chunk-major K order)
-    against the direct LDS-DMA kernel (CLASFV_NO_PATCH_BF16=1, tap-major K order). The two sum the
+    """bf16 stride-1 1x3x3 and 3x1x1 convs: the patch-staged kernel (conv_patch.hip, chunk-major K
+    order) against the direct LDS-DMA kernel (CLASFV_NO_PATCH_BF16=1, tap-major K order). The two sum the
     same bf16 products in different fp32 orders, so bf16 activations may round differently: the
     patch path's error against the fp32 forward must be no larger than the direct path's, and on the
     echo-style clip both stay within the config[4] bar (Dice delta <= 1e-2). The (2,3,16,64,48) case

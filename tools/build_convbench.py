@@ -21,6 +21,7 @@ def main():
     flags = [f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-DCLASFV_KNOCKOUTS", "-I", B.INCLUDE]
     jobs = [(os.path.join(B.CSRC, f), B.EXTRA_FLAGS.get(f, [])) for f in KERNELS]
     jobs.append((os.path.join(HERE, "convbench.hip"), []))
+    jobs.append((os.path.join(HERE, "conv_patch_v1.hip"), []))
 
     def cc(job):
         src, extra = job

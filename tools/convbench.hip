@@ -1,7 +1,9 @@
 // Stand-alone timing of one conv layer shape through the engine's kernels (not part of the product).
 // Build + run (GPU box): bash tools/convbench.sh
 //   convbench KIND N T H W CIN COUT [ITERS] [KO...]
-//   KIND: wino (1x3x3 s1), winot (3x1x1 s1), sp (1x3x3 direct), tp (3x1x1 direct), pw (1x1x1)
+//   KIND: wino (1x3x3 s1), winot (3x1x1 s1), sp (1x3x3 direct), tp (3x1x1 direct), pw (1x1x1),
+//         spp / tpp (bf16 patch-staged 1x3x3 / 3x1x1: ko 0 conv_patch, FR*1000+S*100+NT a conv_patch
+//         variant, 900 conv_dma, 901 the round-1 2-frame kernel, spatial only)
 // KO = knock-out variant of the Winograd kernels (see winograd.hip): timing only, results are wrong.
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -18,6 +20,8 @@ hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winor_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
+hipError_t launch_patch_bf16_v1(const ConvParams& p, hipStream_t s);
+hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
 
 // decoder: N clips of T x H x W, taps at (T, H/2, W/2), (T/2, H/4, W/4), (T/4, H/8), (T/8, H/16)
 static int run_decoder(int N, int T, int H, int W, int iters, const std::vector<int>& kos);
@@ -80,8 +84,8 @@ int main(int argc, char** argv) {
   if (kos.empty()) kos.push_back(0);
   const bool winoq = !strcmp(kind, "winoq"), winor = !strcmp(kind, "winor");
   const bool wino = !strcmp(kind, "wino") || winoq || winor, winot = !strcmp(kind, "winot");
-  const bool spp = !strcmp(kind, "spp");  // bf16 patch-staged 1x3x3 (conv_patch.hip)
-  const bool sp = wino || spp || !strcmp(kind, "sp"), tp = winot || !strcmp(kind, "tp");
+  const bool spp = !strcmp(kind, "spp"), tpp = !strcmp(kind, "tpp");  // bf16 patch-staged (conv_patch.hip)
+  const bool sp = wino || spp || !strcmp(kind, "sp"), tp = winot || tpp || !strcmp(kind, "tp");
   ConvParams p;
   memset(&p, 0, sizeof(p));
   p.N = N, p.Ti = T, p.Hi = H, p.Wi = W, p.Cin = Cin;
@@ -95,7 +99,7 @@ int main(int argc, char** argv) {
     if (tp) p.st = 2, p.To = (T - 1) / 2 + 1;
   }
   // CB_BF16=1: bf16 activations/weights/outputs (direct convs only), K step 32
-  const bool bf = (getenv("CB_BF16") || spp) && !wino && !winot;
+  const bool bf = (getenv("CB_BF16") || spp || tpp) && !wino && !winot;
   p.in_bf16 = p.out_bf16 = bf;
   p.K = p.KT * p.KH * p.KW * Cin;
   p.Kp = bf ? (p.K + 31) / 32 * 32 : (p.K + 15) / 16 * 16;
@@ -123,7 +127,8 @@ int main(int argc, char** argv) {
     else if (winoq) CK(launch_winoq_ko(p, s, ko));
     else if (wino) CK(launch_wino_ko(p, s, ko));
     else if (winot) CK(launch_winot_ko(p, s, ko));
-    else if (spp) CK(launch_patch_bf16(p, s));
+    else if ((spp || tpp) && ko == 901) CK(launch_patch_bf16_v1(p, s));
+    else if ((spp || tpp) && ko != 900) CK(launch_patch_bf16_ko(p, s, ko));
     else {
       int mt, bn;
       conv_pick_tile(p.M, Cout, getenv("CB_NT") ? atoi(getenv("CB_NT")) : 0, &mt, &bn);
