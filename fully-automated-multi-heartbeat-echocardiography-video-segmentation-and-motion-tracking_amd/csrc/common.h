@@ -43,6 +43,7 @@ struct DecParams {
   float* seg;         // (N,2,T,H,W)
   float* mot;         // (N,4,T,H,W)
   int N, T, H, W;
+  int bf16;           // comb_2 on bf16 MFMAs (bf16 engines; taps, heads and outputs stay fp32)
 };
 
 // Launchers (stream-ordered, no synchronisation). Return hipError_t of the launch.
@@ -71,5 +72,9 @@ void winot_transform_weights(const double* w, int cout, int cin, int cout_p, int
 // image.
 bool patch_bf16_supported(const ConvParams& p);
 hipError_t launch_patch_bf16(const ConvParams& p, hipStream_t s);
+// bf16 stem (config[4]): fp32 4-channel clip split into bf16 hi + lo in registers; p.w = hi and lo
+// images, each [64][7][8][4] bf16.
+bool stem_bf16_supported(const ConvParams& p);
+hipError_t launch_stem_bf16(const ConvParams& p, hipStream_t s);
 hipError_t launch_decoder(const DecParams& p, hipStream_t s);
 hipError_t launch_pack_input(const float* x, float* y, int N, int T, int HW, hipStream_t s);

@@ -326,6 +326,119 @@ __global__ __launch_bounds__(256) void conv_stem_f32(ConvParams p, int n_tiles) 
   epilogue<MT, NT>(p, acc, m0 + wid * 32, n0, q, l16);
 }
 
+// bf16 stem for BASELINE config[4] (torchvision R2Plus1dStem conv 1x7x7, stride (1,2,2), padding
+// (0,3,3), 3 -> 45 (64) channels; called from src/model/R2plus1D_18_MotionNet.py:29): the fp32 kernel
+// above runs this conv on fp32 MFMAs, with 64 output channels in bf16 mode. Here the 4-channel fp32
+// clip and the weights are split into bf16 pairs (x = hi + lo) in registers / on the host and
+// multiplied on v_mfma_f32_16x16x32_bf16 as hi.hi + hi.lo + lo.hi (~fp32 accuracy: the stem's
+// rounding would otherwise reach every downstream mask; 3 bf16 MFMAs still cost 3/16 of one fp32):
+//  * K order (kernel row kh, tap kw 0..7 with kw = 7 a zero weight, channel 0..3): one 32-deep K
+//    step per kernel row, and a lane's 8-element A fragment (k group q = taps 2q, 2q+1) is two
+//    horizontally adjacent input pixels = two 16-B loads, straight from global memory (L1/L2: the
+//    stride-2 7x7 windows of neighbouring voxels overlap ~12x);
+//  * the hi and lo 64 x 224 weight images (2 x 28 KB) are staged in LDS once per block, 16-B slots
+//    swizzled by the row (conflict-free ds_read_b128);
+//  * block = 4 waves x 4 m tiles = 256 output voxels x 64 channels per pass, STEM_GROUPS passes per
+//    block (the 56 KB weight staging amortised over 1024 voxels); D^T = W . A^T, so the epilogue
+//    (folded-BN bias, ReLU) stores 8-B bf16 vectors of 4 consecutive channels.
+constexpr int STEM_GROUPS = 1;
+
+__device__ inline bf16x8 stem_bf16x8(f32x4 a, f32x4 b) {
+  return bf16x8{(__bf16)a[0], (__bf16)a[1], (__bf16)a[2], (__bf16)a[3],
+                (__bf16)b[0], (__bf16)b[1], (__bf16)b[2], (__bf16)b[3]};
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_stem_bf16(ConvParams p) {
+  constexpr int MT = 4, NT = 4, ROW = 7 * 64, IMG = 64 * ROW;  // LDS weight row: 7 K steps x 64 B
+  __shared__ __align__(16) char ws[2 * IMG];                    // hi image, lo image
+  const float* x = reinterpret_cast<const float*>(p.x);
+  const char* w16 = reinterpret_cast<const char*>(p.w);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int q = lane >> 4, l16 = lane & 15;
+  const int mb = xcd_swizzle(blockIdx.x, gridDim.x) * 256 * STEM_GROUPS + wid * 64;
+  for (int e = tid; e < 2 * 64 * 28; e += 256) {  // [img][co][kh][slot] 16-B pieces, slot ^ (co & 3)
+    const int im = e / (64 * 28), r0 = e - im * (64 * 28);
+    const int co = r0 / 28, r = r0 - co * 28, kh = r >> 2, sl = r & 3;
+    *reinterpret_cast<uint4*>(ws + im * IMG + co * ROW + kh * 64 + ((sl ^ (co & 3)) << 4)) =
+        *reinterpret_cast<const uint4*>(w16 + (size_t)im * 64 * 448 + (size_t)co * 448 + kh * 64 + sl * 16);
+  }
+  __syncthreads();
+  const int b_rd = l16 * ROW + ((q ^ (l16 & 3)) << 4);
+  for (int g = 0; g < STEM_GROUPS; ++g) {
+    const int m0 = mb + g * 256;
+    // per m tile: input row of kh = 0 and the lane's first column (taps 2q, 2q+1)
+    const float* rowp[MT];
+    int hi0[MT], wi0[MT];
+    bool live[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      int m = m0 + 16 * i + l16;
+      live[i] = m < p.M;
+      if (!live[i]) m = 0;
+      const int wo = m % p.Wo;
+      m /= p.Wo;
+      const int ho = m % p.Ho;
+      const int nt = m / p.Ho;  // n * To + t (stride 1 in time, no temporal padding)
+      hi0[i] = 2 * ho - 3;
+      wi0[i] = 2 * wo - 3 + 2 * q;
+      rowp[i] = x + ((size_t)nt * p.Hi * p.Wi) * 4;
+    }
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+      bf16x8 ah[MT], al[MT], bh[NT], bl[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int hi = hi0[i] + kh;
+        const bool rok = live[i] && (unsigned)hi < (unsigned)p.Hi;
+        const float* px = rowp[i] + ((size_t)hi * p.Wi + wi0[i]) * 4;
+        f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+        if (rok && (unsigned)wi0[i] < (unsigned)p.Wi) v0 = *reinterpret_cast<const f32x4*>(px);
+        if (rok && (unsigned)(wi0[i] + 1) < (unsigned)p.Wi) v1 = *reinterpret_cast<const f32x4*>(px + 4);
+        ah[i] = stem_bf16x8(v0, v1);
+        f32x4 r0, r1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          r0[e] = v0[e] - (float)ah[i][e];
+          r1[e] = v1[e] - (float)ah[i][4 + e];
+        }
+        al[i] = stem_bf16x8(r0, r1);
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        bh[j] = *reinterpret_cast<const bf16x8*>(ws + j * 16 * ROW + kh * 64 + b_rd);
+        bl[j] = *reinterpret_cast<const bf16x8*>(ws + IMG + j * 16 * ROW + kh * 64 + b_rd);
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], ah[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], al[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], ah[i], acc[i][j], 0, 0, 0);
+        }
+    }
+    __bf16* y = reinterpret_cast<__bf16*>(p.y);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      if (!live[i]) continue;
+      const size_t m = (size_t)m0 + 16 * i + l16;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = 16 * j + 4 * q;
+        f32x4 v = acc[i][j] + *reinterpret_cast<const f32x4*>(p.bias + n);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        *reinterpret_cast<bf16x4*>(y + m * 64 + n) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+      }
+    }
+  }
+}
+
 template <typename T, int MT, int NT, int S>
 hipError_t launch_dma(const ConvParams& p, hipStream_t s) {
   constexpr int BM = 64 * MT, BN = 16 * NT;
@@ -418,3 +531,17 @@ hipError_t launch_pack_input(const float* x, float* y, int N, int T, int HW, hip
   hipLaunchKernelGGL(pack_input_kernel, dim3(blocks), dim3(256), 0, s, x, y, N, T, HW);
   return hipGetLastError();
 }
+
+bool stem_bf16_supported(const ConvParams& p) {
+  return p.stem && p.out_bf16 && p.Cin == 4 && p.Cout == 64 && p.KT == 1 && p.KH == 7 && p.KW == 7 && p.st == 1 &&
+         p.sh == 2 && p.sw == 2 && p.pt == 0 && p.ph == 3 && p.pw == 3 && p.relu && !p.res && p.bias &&
+         p.To == p.Ti && (size_t)p.M < ((size_t)1 << 31);
+}
+
+// p.w: hi then lo image, each [64][7 kh][8 kw][4 c] bf16 (engine.hip, clasfv_finalize).
+hipError_t launch_stem_bf16(const ConvParams& p, hipStream_t s) {
+  if (!stem_bf16_supported(p)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(conv_stem_bf16, dim3((p.M + 256 * STEM_GROUPS - 1) / (256 * STEM_GROUPS)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+

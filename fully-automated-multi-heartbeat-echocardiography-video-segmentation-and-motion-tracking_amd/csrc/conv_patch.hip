@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     ConvParams p, int n_tiles, int ptw, int npt, int t_tiles) {
   using G = PGeo<KT, FR>;
   constexpr int TAPS = G::TAPS, MT = G::MT;
-  static_assert(S >= 3 && S <= TAPS + 1, "wait counts below assume S - 1 <= TAPS");
+  static_assert(S >= 2 && S <= TAPS + 1, "wait counts below assume S - 1 <= TAPS");
   constexpr int PW = (G::PIECES + 3) / 4, BW = (NT + 3) / 4;  // DMAs per wave (uniform counts)
   constexpr int B_STAGE = NT * 1024, B0 = 2 * G::BYTES, SINK = B0 + S * B_STAGE;
   constexpr int LDS = SINK + 1024;
@@ -301,23 +301,29 @@ hipError_t launch_p(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Output frames per block: 2 for the 1x3x3 convs (3 blocks per CU at NT <= 5), 4 for the 3x1x1
-// convs (the 6-frame patch halves the temporal halo's re-fetch against 2 frames; tools/bench_patch.sh).
+// Output frames per block and B ring depth (tools/bench_patch.sh): 1x3x3 convs 2 frames, 2 stages
+// (a 2-deep ring measured as fast as 3-5 stages and leaves the LDS for 3 blocks per CU at NT = 10);
+// 3x1x1 convs 4 frames (the 6-frame patch halves the temporal halo's re-fetch against 2 frames), 3
+// stages.
 template <int KT>
 constexpr int product_fr() {
   return KT == 1 ? 2 : 4;
 }
+template <int KT>
+constexpr int product_s() {
+  return KT == 1 ? 2 : 3;
+}
 
 template <int KT>
 hipError_t launch_nt(const ConvParams& p, int nt, hipStream_t s) {
-  constexpr int FR = product_fr<KT>();
+  constexpr int FR = product_fr<KT>(), S = product_s<KT>();
   switch (nt) {
-    case 10: return launch_p<10, KT, FR>(p, s);
-    case 9: return launch_p<9, KT, FR>(p, s);
-    case 8: return launch_p<8, KT, FR>(p, s);
-    case 6: return launch_p<6, KT, FR>(p, s);
-    case 5: return launch_p<5, KT, FR>(p, s);
-    case 4: return launch_p<4, KT, FR>(p, s);
+    case 10: return launch_p<10, KT, FR, S>(p, s);
+    case 9: return launch_p<9, KT, FR, S>(p, s);
+    case 8: return launch_p<8, KT, FR, S>(p, s);
+    case 6: return launch_p<6, KT, FR, S>(p, s);
+    case 5: return launch_p<5, KT, FR, S>(p, s);
+    case 4: return launch_p<4, KT, FR, S>(p, s);
   }
   return hipErrorInvalidValue;
 }
@@ -372,6 +378,9 @@ template <int KT, int FR, int S>
 hipError_t ko_nt(const ConvParams& p, int nt, hipStream_t s) {
   switch (nt) {
     case 10: if constexpr (patch_occ<10, KT, FR, S>() >= 1) return launch_p<10, KT, FR, S>(p, s); break;
+    case 9: if constexpr (patch_occ<9, KT, FR, S>() >= 1) return launch_p<9, KT, FR, S>(p, s); break;
+    case 8: if constexpr (patch_occ<8, KT, FR, S>() >= 1) return launch_p<8, KT, FR, S>(p, s); break;
+    case 6: return launch_p<6, KT, FR, S>(p, s);
     case 5: return launch_p<5, KT, FR, S>(p, s);
     case 4: return launch_p<4, KT, FR, S>(p, s);
   }
@@ -380,6 +389,7 @@ hipError_t ko_nt(const ConvParams& p, int nt, hipStream_t s) {
 template <int KT, int FR>
 hipError_t ko_s(const ConvParams& p, int st, int nt, hipStream_t s) {
   switch (st) {
+    case 2: return ko_nt<KT, FR, 2>(p, nt, s);
     case 3: return ko_nt<KT, FR, 3>(p, nt, s);
     case 4: return ko_nt<KT, FR, 4>(p, nt, s);
   }

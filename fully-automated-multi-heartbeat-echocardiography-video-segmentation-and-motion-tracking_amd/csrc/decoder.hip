@@ -1,4 +1,5 @@
-// Fused full-resolution CLAS-FV decoder for gfx950.
+// Fused full-resolution CLAS-FV decoder for gfx950 (fp32; bf16 MFMAs for comb_2 and the heads in
+// bf16 engines: comb_2 on bf16 MFMAs).
 //
 // Reference (src/model/R2plus1D_18_MotionNet.py:39-71): five trilinear align_corners=True
 // upsamplings of the encoder taps to (T,H,W), torch.cat to 1024 channels (1.64 GB at 32x112x112),
@@ -65,8 +66,99 @@ __device__ inline int xcd_swizzle_d(int b, int nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ inline bf16x8 to_bf16x8(f32x4 a, f32x4 b) {
+  return bf16x8{(__bf16)a[0], (__bf16)a[1], (__bf16)a[2], (__bf16)a[3],
+                (__bf16)b[0], (__bf16)b[1], (__bf16)b[2], (__bf16)b[3]};
+}
+
+// x = hi + lo with hi = bf16(x), lo = bf16(x - hi): the pair carries ~16 mantissa bits
+__device__ inline void split_bf16x8(f32x4 a, f32x4 b, bf16x8& hi, bf16x8& lo) {
+  hi = to_bf16x8(a, b);
+  f32x4 ra, rb;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    ra[e] = a[e] - (float)hi[e];
+    rb[e] = b[e] - (float)hi[4 + e];
+  }
+  lo = to_bf16x8(ra, rb);
+}
+
+// Steps 3-5 of the bf16-engine decoder (see decoder_kernel): h1[mt][c][j] = channel 16c + 4q + j of
+// voxel (row h0 + 2 wid + mt, column w0 + l16). comb_2 runs as three bf16 products per K block
+// (hi.hi + hi.lo + lo.hi of the split operands: ~fp32 accuracy at 6 instead of 32 MFMA slots).
+__device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[2][4], int t, int n, int h0, int w0,
+                                          int wid, int q, int l16) {
+  bf16x8 hh[2][2], hl[2][2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) split_bf16x8(h1[mt][2 * kb], h1[mt][2 * kb + 1], hh[mt][kb], hl[mt][kb]);
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const float* wr = p.w2 + (16 * nt + l16) * 64 + 4 * q;
+    bf16x8 wh_[2], wl_[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      split_bf16x8(*reinterpret_cast<const f32x4*>(wr + 32 * kb), *reinterpret_cast<const f32x4*>(wr + 32 * kb + 16),
+                   wh_[kb], wl_[kb]);
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl_[kb], hh[mt][kb], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh_[kb], hl[mt][kb], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh_[kb], hh[mt][kb], a, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = fmaxf(a[r] + bb[r], 0.f);
+      acc[mt][nt] = a;  // h2^T[ch = 16nt + 4q + r][voxel l16]
+    }
+  }
+  // heads in fp32 (they produce the logits whose sign is the mask): heads^T = Wh . h2^T on
+  // v_mfma_f32_16x16x4_f32, the accumulator layout being the B operand layout (k = 16nt + 4q + r)
+  f32x4 wh[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    wh[nt] = *reinterpret_cast<const f32x4*>(p.wh + (l16 & 7) * 64 + 16 * nt + 4 * q);
+    if (l16 >= 8) wh[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const size_t HW = (size_t)p.H * p.W;
+  const size_t TH = (size_t)p.T * HW;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int hr = h0 + 2 * wid + mt;
+    f32x4 out = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[mt][nt][r], out, 0, 0, 0);
+    if (q < 2) {
+      const size_t pix = (size_t)t * HW + (size_t)hr * p.W + (w0 + l16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 4 * q + r;
+        if (co >= 6) continue;
+        const float v = out[r] + p.bh[co];
+        if (co < 2)
+          p.seg[((size_t)n * 2 + co) * TH + pix] = v;
+        else
+          p.mot[((size_t)n * 4 + (co - 2)) * TH + pix] = tanhf(v);
+      }
+    }
+  }
+}
+
 // (Heads as VALU dot products + a 4-lane-group reduction instead of the 16-row head MFMA of which 6
 // rows are used measured slower: 1.83 vs 1.70 ms per 30 clips -- the interpolation already loads VALU.)
+// BF = 1 (BASELINE config[4]): comb_2 on v_mfma_f32_16x16x32_bf16 with split (hi + lo) bf16 h1 and W2
+// (one 32-deep K block = the 8 channels 16c + 4q + j, c in {2kb, 2kb+1}, that lane group q already
+// holds, so both operands keep the fp32 path's register layout), fp32 accumulation; fp32 heads.
+template <int BF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void decoder_kernel(DecParams p) {
   extern __shared__ __align__(16) float smem[];
   float* stage = smem;  // STAGE_FLOATS
@@ -201,6 +293,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
       for (int j = 0; j < 4; ++j) h1[mt][c][j] = fmaxf(h1[mt][c][j], 0.f);
   }
 
+  if constexpr (BF) {
+    decoder_heads_bf16(p, h1, t, n, h0, w0, wid, q, l16);
+    return;
+  }
   // 3. h2^T[n][v] = sum_k W2[n][k] h1[v][k]; MFMA j of lane group q covers k = 16c + 4q + j
   // (W2 rows of the next 16-channel tile are prefetched while the current one runs on MFMA)
   f32x4 acc[2][4], wa[4], wn[4];
@@ -272,12 +368,16 @@ static hipError_t launch_dec(const DecParams& p, hipStream_t s) {
   const size_t lds = (size_t)STAGE_FLOATS * 4;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)decoder_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
-    if (e != hipSuccess) return e;
+    for (const void* k : {(const void*)decoder_kernel<0>, (const void*)decoder_kernel<1>}) {
+      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
     attr_set = true;
   }
-  hipLaunchKernelGGL(decoder_kernel, dim3((unsigned)nb), dim3(256), lds, s, p);
+  if (p.bf16)
+    hipLaunchKernelGGL(decoder_kernel<1>, dim3((unsigned)nb), dim3(256), lds, s, p);
+  else
+    hipLaunchKernelGGL(decoder_kernel<0>, dim3((unsigned)nb), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 

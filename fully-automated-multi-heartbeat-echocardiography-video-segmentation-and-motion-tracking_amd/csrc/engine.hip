@@ -80,6 +80,7 @@ struct Conv {
   float* dwino = nullptr;  // Winograd F(2x2,3x3) transformed weights (fp32 stride-1 1x3x3 convs)
   float* dwinor = nullptr;  // Winograd F(2x4,3x3) transformed weights (the same convs, Cin <= 128)
   float* dwinot = nullptr;  // Winograd F(4,3)-in-time transformed weights (fp32 stride-1 3x1x1 convs)
+  void* dws16 = nullptr;    // bf16 stem weights, hi and lo images [64][7 kh][8 kw][4 c] (bf16 engines)
 };
 
 // fp32 stride-1 1x3x3 convs run on the fused Winograd kernel unless CLASFV_WINOGRAD=0.
@@ -303,6 +304,8 @@ double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
     return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 1) / 2) * 16.0 * cc * 1e-9;
   if (!strcmp(kname, "conv_wino_r")) return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 3) / 4) * 24.0 * cc * 1e-9;
   if (!strcmp(kname, "conv_winot")) return 2.0 * out.n * (out.t / 4) * (double)out.h * out.w * 6.0 * cc * 1e-9;
+  if (!strcmp(kname, "conv_stem_bf16"))
+    return 3 * 2.0 * ceil((double)out.n * out.t * out.h * out.w / 256.0) * 256.0 * 64.0 * 224.0 * 1e-9;
   if (!strcmp(kname, "conv_patch_bf16")) {  // frames x 64-pixel tiles: 2 x 8x8 for 1x3x3, 4 x 64 flat for 3x1x1
     const int fr = c.kt == 1 ? 2 : 4;
     const double px = c.kt == 1 ? (double)((out.h + 7) / 8 * 8) * ((out.w + 7) / 8 * 8)
@@ -361,6 +364,13 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
       return CLASFV_OK;
     }
     p.w = c.dw;
+  }
+  static const bool no_stem_bf16 = getenv("CLASFV_NO_STEM_BF16") != nullptr;  // A/B switch (tests)
+  if (c.dws16 && !no_stem_bf16 && stem_bf16_supported(p)) {
+    p.w = c.dws16;
+    HIP_TRY(launch_stem_bf16(p, s));
+    *kname = "conv_stem_bf16";
+    return CLASFV_OK;
   }
   if (c.dwinot) {
     p.w = c.dwinot;
@@ -489,6 +499,7 @@ int clasfv_destroy(clasfv_t h) {
     (void)hipFree(c.dwino);
     (void)hipFree(c.dwinor);
     (void)hipFree(c.dwinot);
+    (void)hipFree(c.dws16);
   }
   for (auto& c : h->proj) (void)hipFree(c.dw);
   (void)hipFree(h->b1);
@@ -550,7 +561,9 @@ int clasfv_finalize(clasfv_t h) {
     (void)hipFree(c.dwino);
     (void)hipFree(c.dwinor);
     (void)hipFree(c.dwinot);
-    c.dw = c.db = nullptr;
+    (void)hipFree(c.dws16);
+    c.dw = c.dws16 = nullptr;
+    c.db = nullptr;
     c.dwino = c.dwinor = c.dwinot = nullptr;
     bn_scale_shift(h, c.bn, c.cout, s, t);
     const auto& w = P(h, c.w + ".weight");
@@ -571,6 +584,23 @@ int clasfv_finalize(clasfv_t h) {
         winor_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, ur.data());
         if ((rc = upload(ur, &c.dwinor))) return rc;
       }
+    }
+    if (bf16 && c.stem && c.cout_p == 64 && c.kh == 7 && c.kw == 7 && cin <= 4) {  // conv_stem_bf16's K order
+      const size_t img = (size_t)64 * 7 * 8 * 4;
+      std::vector<float> ws(2 * img, 0.f);  // hi image, then lo = bf16(w - hi)
+      for (int o = 0; o < c.cout; ++o)
+        for (int ci = 0; ci < cin; ++ci)
+          for (int kh = 0; kh < 7; ++kh)
+            for (int kw = 0; kw < 7; ++kw) {
+              const float v = (float)((double)w[((size_t)o * cin + ci) * 49 + kh * 7 + kw] * s[o]);
+              const uint32_t hb = (uint32_t)to_bf16(v) << 16;
+              float hi;
+              memcpy(&hi, &hb, 4);
+              const size_t k = (((size_t)o * 7 + kh) * 8 + kw) * 4 + ci;
+              ws[k] = hi;
+              ws[img + k] = v - hi;
+            }
+      if ((rc = upload_bf16(ws, &c.dws16))) return rc;
     }
     if (use_winot(c, bf16)) {
       std::vector<double> wf((size_t)c.cout * cin * 3);
@@ -738,7 +768,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   if ((rc = run(h->proj[3], taps[3], taps_shape[3], buf(PP3), sp3, nullptr, false))) return rc;
   if ((rc = run(h->proj[4], taps[4], taps_shape[4], buf(PP4), sp4, nullptr, false))) return rc;
 
-  DecParams d;
+  DecParams d{};
   const Shape5 tsh[4] = {sp, sp2, sp3, sp4};
   const int tb[4] = {P01, PP2, PP3, PP4};
   for (int i = 0; i < 4; ++i) {
@@ -758,10 +788,13 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   d.seg = seg;
   d.mot = mot;
   d.N = N, d.T = T, d.H = H, d.W = W;
+  static const bool no_dec_bf16 = getenv("CLASFV_NO_DECODER_BF16") != nullptr;  // A/B switch (tests)
+  d.bf16 = h->dtype == CLASFV_DTYPE_BF16 && !no_dec_bf16;
   HIP_TRY(launch_decoder(d, s));
-  // comb_2 (64x64) and the heads (6 useful of the 16 rows of their MFMA tile) per output voxel
+  // comb_2 (64x64; three split-bf16 products in bf16 engines) and the heads (6 useful of the 16 rows
+  // of their MFMA tile) per output voxel
   timed("decoder_kernel", 2.0 * N * (double)T * H * W * (64 * 64 + 64 * 6) * 1e-9,
-        2.0 * N * (double)T * H * W * (64 * 64 + 64 * 16) * 1e-9);
+        2.0 * N * (double)T * H * W * ((d.bf16 ? 3 : 1) * 64 * 64 + 64 * 16) * 1e-9);
   return CLASFV_OK;
 }
 

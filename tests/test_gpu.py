@@ -5,6 +5,8 @@ folded BatchNorm, decoder commuted to project-then-interpolate), so raw logits a
 absolute tolerance and the derived masks with the north_star bar Dice delta <= 1e-3. Plumbing
 kernels (clip building, resample, argmax, voting, normaliser) are compared bit for bit.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -16,6 +18,7 @@ from tests.golden.fake_model import fake_model
 pytestmark = pytest.mark.gpu
 
 DICE_TOL = 1e-3
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def dice_delta(a, b):
@@ -476,6 +479,50 @@ def test_bf16_patch_conv_matches_direct_conv(model, monkeypatch, shape):
     assert (lab_p == lab32).mean() >= 0.99
     if shape[2:] == (32, 112, 112):
         assert lab32.sum() > 1000 and dice_delta(lab_p, lab32) <= 1e-2
+
+
+@pytest.mark.parametrize("switch", ["CLASFV_NO_STEM_BF16", "CLASFV_NO_DECODER_BF16"])
+def test_bf16_stem_and_decoder_vs_fp32_mfma_forms(switch):
+    """config[4]: the bf16 stem (conv.hip conv_stem_bf16: clip rounded to bf16, bf16 MFMAs) and the
+    bf16 decoder heads (decoder.hip, comb_2 + heads on bf16 MFMAs) against their fp32-MFMA forms
+    (switch set; read once per process, so each form runs in a subprocess). The default bf16
+    forward must stay within the config[4] bar of the fp32 forward, with an error no larger than a
+    small margin over the fp32-MFMA form's."""
+    import subprocess
+    import sys
+    import tempfile
+    code = (
+        "import numpy as np, torch, sys\n"
+        "sys.path.insert(0, %r)\n"
+        "import clasfv_amd.synthetic as S\n"
+        "from clasfv_amd.model import R2plus1D_18_MotionNet\n"
+        "from oracle import fuse_ref\n"
+        "v = fuse_ref.zeroone_normalizer(S.echo_video(64, seed=3))\n"
+        "x = torch.from_numpy(np.ascontiguousarray(v[None, :, 10:42]))\n"
+        "m = R2plus1D_18_MotionNet(pretrained=False, dtype='bf16')\n"
+        "s, mo = m(x)\n"
+        "np.save(sys.argv[1], np.concatenate([s.cpu().numpy().ravel(), mo.cpu().numpy().ravel()]))\n" % REPO)
+    outs = {}
+    for name, env in (("default", {}), ("fp32_form", {switch: "1"})):
+        with tempfile.NamedTemporaryFile(suffix=".npy") as f:
+            r = subprocess.run([sys.executable, "-c", code, f.name], env=dict(os.environ, **env), capture_output=True,
+                               text=True, timeout=300)
+            assert r.returncode == 0, r.stderr[-2000:]
+            outs[name] = np.load(f.name)
+    import clasfv_amd.synthetic as S
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    v = fuse_ref.zeroone_normalizer(S.echo_video(64, seed=3))
+    x = torch.from_numpy(np.ascontiguousarray(v[None, :, 10:42]))
+    s32, m32 = R2plus1D_18_MotionNet(pretrained=False)(x)
+    ref = np.concatenate([s32.cpu().numpy().ravel(), m32.cpu().numpy().ravel()])
+    e_d = np.abs(outs["default"] - ref)
+    e_f = np.abs(outs["fp32_form"] - ref)
+    assert np.isfinite(outs["default"]).all()
+    assert np.median(e_d) <= 1.5 * np.median(e_f) + 1e-3, (np.median(e_d), np.median(e_f))
+    seg = outs["default"][: s32.numel()].reshape(s32.shape)
+    lab = (seg[:, 1] > seg[:, 0]).ravel()
+    lab32 = (s32[:, 1] > s32[:, 0]).cpu().numpy().ravel()
+    assert lab32.sum() > 1000 and dice_delta(lab, lab32) <= 1e-2
 
 
 @pytest.mark.parametrize("shape", [(1, 3, 32, 112, 112), (2, 3, 16, 64, 48)])
