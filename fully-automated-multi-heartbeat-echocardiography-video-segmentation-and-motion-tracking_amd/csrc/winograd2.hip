@@ -46,8 +46,13 @@ template <int PT>
 struct QPatch {
   static constexpr int SIDE = 2 * PT + 2;                 // input patch side (pixels)
   static constexpr int PIX = SIDE * SIDE;
+  // pixels between the patches of a raw stage. PT = 4: 101 (one pad pixel), so that the transform's
+  // wave (one tile row ly of both patches: 4 lx x 2 patches x 8 channels) reads pixels whose 32-B
+  // slots fall in 8 distinct bank groups: 2 lx + 5 pp (mod 8). At a 100-pixel stride every
+  // transform ds_read_b32 and V write was 2-way bank-conflicted.
+  static constexpr int PSTRIDE = PT == 4 ? PIX + 1 : PIX;
   static constexpr int PPB = Q_BT / (PT * PT);            // patches per block
-  static constexpr int SLOTS = PPB * PIX * 2;             // 16-B DMA slots per chunk (8 channels)
+  static constexpr int SLOTS = PPB * PSTRIDE * 2;         // 16-B DMA slots per chunk (8 channels)
   static constexpr int DPW = ((SLOTS + 63) / 64 + 3) / 4;  // DMAs per wave per chunk
   // raw stage = all 4*DPW wave-instructions when that still fits 2 blocks per CU, otherwise only the
   // ones carrying data, the rest landing in a 1 KB sink
@@ -80,17 +85,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int PY = H / (2 * PT), PX = W / (2 * PT);
   const int nchunk = NCH > 0 ? NCH : C >> 3;
 
-  // raw DMA: instruction j of this wave fills slots s = (wid + 4j)*64 + lane, s = pp*2*PIX + pix*2 + half
+  // raw DMA: instruction j of this wave fills slots s = (wid + 4j)*64 + lane, s = pp*2*PSTRIDE + pix*2 + half
   int d_off[DPW];
 #pragma unroll
   for (int j = 0; j < DPW; ++j) {
     const int s = (wid + 4 * j) * 64 + lane;
     int off = -1;
     if (s < G::SLOTS) {
-      const int pp = s / (2 * G::PIX), rem = s - pp * (2 * G::PIX), pix = rem >> 1, half = rem & 1;
+      const int pp = s / (2 * G::PSTRIDE), rem = s - pp * (2 * G::PSTRIDE), pix = rem >> 1, half = rem & 1;
       const int py = pix / G::SIDE, px = pix - py * G::SIDE;
       const int gp = pg0 + pp;
-      if (gp < n_patches) {
+      if (gp < n_patches && pix < G::PIX) {
         const int f = gp / (PY * PX), r = gp - f * (PY * PX);
         const int pr = r / PX, pc = r - pr * PX;
         const int yy = pr * 2 * PT - 1 + py, xx = pc * 2 * PT - 1 + px;
@@ -117,8 +122,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int h = 0; h < 2; ++h) u[nt][h] = *reinterpret_cast<const f32x4*>(b + (size_t)nt * 16 * 32 + h * 4);
   };
   // transform thread = (tile tt = pp*PT*PT + ly*PT + lx, channel cc)
-  const int tt = tid >> 3, cc = tid & 7;
-  const int raw_off = (tt / (PT * PT)) * G::PIX * 8 + (2 * ((tt / PT) % PT) * G::SIDE + 2 * (tt % PT)) * 8 + cc;
+  // (PT = 4: wave = tile row ly of both patches, lane = (patch, lx, channel); PT = 2: 8 consecutive tiles)
+  const int tt = PT == 4 ? (lane >> 5) * 16 + wid * 4 + ((lane >> 3) & 3) : tid >> 3, cc = tid & 7;
+  const int raw_off = (tt / (PT * PT)) * G::PSTRIDE * 8 + (2 * ((tt / PT) % PT) * G::SIDE + 2 * (tt % PT)) * 8 + cc;
   const int v_off = (((tt & 15) * 4 + (cc >> 1)) * 2 + (tt >> 4)) * 2 + (cc & 1);  // V[e][tile&15][ci>>1][pp][ci&1]
   auto transform_read = [&](int rstage, float (&d)[16]) __attribute__((always_inline)) {
     const float* rb = reinterpret_cast<const float*>(raw + rstage * Q_RAW) + raw_off;
