@@ -463,6 +463,9 @@ hipError_t winot5_dispatch(const ConvParams& p, hipStream_t s, int force_nt = 0)
   return nt == 4 ? winot5_launch<2, 4>(p, s) : winot5_launch<2, 2>(p, s);
 }
 
+// conv_winot5 addresses its input with 32-bit byte offsets from the chunk's scalar base
+bool winot5_fits(const ConvParams& p) { return (size_t)p.N * p.Ti * p.Hi * p.Wi * p.Cin * 4 < ((size_t)1 << 32); }
+
 }  // namespace
 
 bool winot_supported(const ConvParams& p) {
@@ -479,7 +482,7 @@ hipError_t launch_winot(const ConvParams& p, hipStream_t s) {
   // the same order (bit-identical outputs). conv_winot5 needs T % 8 == 0 (whole tile pairs);
   // layer4 at 32-frame clips (T = 4, fewer than 256 blocks) stays on conv_winot.
   const bool reference = getenv("CLASFV_WINOT_REFERENCE") != nullptr;
-  if (!reference && p.Ti % 8 == 0) return winot5_dispatch(p, s);
+  if (!reference && p.Ti % 8 == 0 && winot5_fits(p)) return winot5_dispatch(p, s);
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)conv_winot, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
