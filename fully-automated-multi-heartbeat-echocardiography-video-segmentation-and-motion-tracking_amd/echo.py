@@ -24,6 +24,8 @@ Pinned by tests/golden/ef.npz, which the reference code itself produced (tests/g
 """
 from concurrent.futures import ThreadPoolExecutor
 
+import warnings
+
 import numpy as np
 from scipy.signal import find_peaks
 
@@ -44,7 +46,8 @@ def get2dPucks(abin, apix, npucks=10):
         return 1.0, np.zeros((npucks,))
     spacing = np.asarray(apix, dtype=np.float64).reshape(2, 1)
     pts = np.stack(np.nonzero(mask)) * spacing            # (2, n) pixel coordinates
-    with np.errstate(invalid="ignore", divide="ignore"):
+    with np.errstate(invalid="ignore", divide="ignore"), warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)  # one-pixel masks: "Degrees of freedom <= 0"
         cov = np.cov(pts, rowvar=True)
     try:  # a one-pixel mask has an undefined (NaN) covariance: (0.0, zeros) as the reference
         evals, evecs = np.linalg.eig(cov)
