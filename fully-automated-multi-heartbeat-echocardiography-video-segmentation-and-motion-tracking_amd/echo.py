@@ -22,9 +22,8 @@ Behaviour (not code) of the reference's EF stage, re-derived from SURVEY.md sect
 
 Pinned by tests/golden/ef.npz, which the reference code itself produced (tests/golden/make_golden_ef.py).
 """
-from concurrent.futures import ThreadPoolExecutor
-
 import warnings
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 from scipy.signal import find_peaks
