@@ -22,6 +22,7 @@ def main():
     jobs = [(os.path.join(B.CSRC, f), B.EXTRA_FLAGS.get(f, [])) for f in KERNELS]
     jobs.append((os.path.join(HERE, "convbench.hip"), []))
     jobs.append((os.path.join(HERE, "conv_patch_v1.hip"), []))
+    jobs.append((os.path.join(HERE, "winoq_probe.hip"), []))
 
     def cc(job):
         src, extra = job

@@ -22,6 +22,7 @@ hipError_t launch_winor_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
 hipError_t launch_patch_bf16_v1(const ConvParams& p, hipStream_t s);
 hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
+hipError_t launch_winoq_probe(const ConvParams& p, hipStream_t s, int ko);
 
 // decoder: N clips of T x H x W, taps at (T, H/2, W/2), (T/2, H/4, W/4), (T/4, H/8), (T/8, H/16)
 static int run_decoder(int N, int T, int H, int W, int iters, const std::vector<int>& kos);
@@ -82,7 +83,8 @@ int main(int argc, char** argv) {
   std::vector<int> kos;
   for (int i = 9; i < argc; ++i) kos.push_back(atoi(argv[i]));
   if (kos.empty()) kos.push_back(0);
-  const bool winoq = !strcmp(kind, "winoq"), winor = !strcmp(kind, "winor");
+  const bool winoqp = !strcmp(kind, "winoqp");  // conv_wino_q knock-out probes (tools/winoq_probe.hip)
+  const bool winoq = !strcmp(kind, "winoq") || winoqp, winor = !strcmp(kind, "winor");
   const bool wino = !strcmp(kind, "wino") || winoq || winor, winot = !strcmp(kind, "winot");
   const bool spp = !strcmp(kind, "spp"), tpp = !strcmp(kind, "tpp");  // bf16 patch-staged (conv_patch.hip)
   const bool sp = wino || spp || !strcmp(kind, "sp"), tp = winot || tpp || !strcmp(kind, "tp");
@@ -124,6 +126,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&b));
   auto launch = [&](int ko) {
     if (winor) CK(launch_winor_ko(p, s, ko));
+    else if (winoqp) CK(launch_winoq_probe(p, s, ko));
     else if (winoq) CK(launch_winoq_ko(p, s, ko));
     else if (wino) CK(launch_wino_ko(p, s, ko));
     else if (winot) CK(launch_winot_ko(p, s, ko));

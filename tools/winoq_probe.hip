@@ -12,7 +12,7 @@
 // 8x8-pixel patches (PT = 4 tiles per side); maps with Ho, Wo % 4 == 0 (layer2 at 112x112 clips:
 // 28x28) use 4x4-pixel patches (PT = 2: 8 patches of 6x6 input pixels per block, 1.78x fewer raw
 // bytes than per-tile windows; layer2 128->288: conv_wino 1.32 -> 1.18 ms).
-#include "common.h"
+#include "../fully-automated-multi-heartbeat-echocardiography-video-segmentation-and-motion-tracking_amd/csrc/common.h"
 
 namespace {
 
@@ -64,14 +64,24 @@ struct QPatch {
 static_assert(QPatch<4>::LDS == 72 * 1024 && QPatch<4>::DPW == 2, "PT = 4 layout");
 static_assert(QPatch<2>::DPW == 3 && QPatch<2>::LDS <= 80 * 1024, "PT = 2 layout: 2 blocks per CU");
 
-// EPI: epilogue form, bit 0 = residual add, bit 1 = ReLU (compile-time: as runtime flags every
-// output element carried two selects).
-template <int NCH, int PT = 4, int EPI = 2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino_q(ConvParams p, int n_co,
+template <int NCH, int PT = 4, int KO = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino_q_probe(ConvParams p, int n_co,
                                                                                              int n_patches) {
   using G = QPatch<PT>;
   constexpr int Q_RAW = G::RAW, DPW = G::DPW;
   __shared__ __align__(16) char smem[G::LDS];
+  if constexpr ((KO & 256) != 0) {  // stagger: the second wave of first-round blocks starts ~half a block late
+    if (blockIdx.x >= 256 && blockIdx.x < 512) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+  }
+  if constexpr ((KO & 512) != 0) {  // stagger by block parity of the first round
+    if (blockIdx.x < 512 && (blockIdx.x & 1)) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+  }
   char* raw = smem;
   char* vbuf = smem + 3 * Q_RAW;
   char* sink = smem + 3 * Q_RAW + 3 * Q_V;  // DMAs past NINSTR (PT = 2) land here
@@ -177,6 +187,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // transform raw(1). Per chunk each wave then issues exactly 2 DMAs + 6 U loads (past-the-end
   // fetches read the zero block / chunk 0), so the counted vmcnt values are exact.
   // (the sched_barriers pin the issue order the counted vmcnt relies on)
+  if constexpr (!(KO & 128)) {
   issue_raw(0, 0);
   __builtin_amdgcn_sched_barrier(0);
   issue_raw(1, 1);
@@ -210,23 +221,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+  } else {
+    load_u(0, uu[0]);
+    load_u(1, uu[1]);
+  }
   read_a(0, aa[0]);
 
   auto step = [&](int k, f32x4 (&uc)[3][2], f32x4 (&un)[3][2], f32x4 (&ac)[4], f32x4 (&an)[4])
                   __attribute__((always_inline)) {
     // vmcnt(DPW + 6): raw(k+2), U(k) landed; lgkmcnt(0): own V stores and operand reads done
-    __builtin_amdgcn_s_waitcnt(0x0070 | (DPW + 6));
+    if constexpr (!(KO & 2)) __builtin_amdgcn_s_waitcnt(0x0070 | (DPW + 6));
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
+    if constexpr (!(KO & 1)) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    // raw(k+4) LDS-DMAs before this chunk's LDS reads: issued after them, the compiler drains the
-    // reads (lgkmcnt(0)) in front of the DMA, which stalls the wave's MFMA stream
-    issue_raw(k + 4, (k + 1) % 3);
+    if constexpr (!(KO & 8)) issue_raw(k + 4, (k + 1) % 3);
     __builtin_amdgcn_sched_barrier(0);
-    read_a((k + 1) % 3, an);
-    float d[16];  // raw(k+2) -> V((k+2)%3); branch-free (the last chunks transform unused fetches)
-    transform_read((k + 2) % 3, d);
-    load_u(k + 2, un);
+    if constexpr (!(KO & 32)) read_a((k + 1) % 3, an);
+    float d[16];
+    if constexpr (!(KO & 4)) transform_read((k + 2) % 3, d);
+    else for (int i = 0; i < 16; ++i) d[i] = (float)i;
+    if constexpr (!(KO & 16)) load_u(k + 2, un);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -238,7 +252,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             acc[j][m][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[j][2 * m + s2], uc[nt][j >> 1][(j & 1) * 2 + s2],
                                                                  acc[j][m][nt], 0, 0, 0);
           }
-    transform_write(d, (k + 2) % 3);
+    if constexpr (!(KO & 4)) transform_write(d, (k + 2) % 3);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -276,9 +290,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // drain past-the-end fetches before LDS is reused
 
+  if constexpr ((KO & 64) != 0) {  // keep the accumulators alive without the epilogue
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int nt = 0; nt < 3; ++nt) t += acc[j][m][nt][0] + acc[j][m][nt][3];
+    if (t == 1234.5f) reinterpret_cast<float*>(p.y)[tid] = t;
+    return;
+  }
   // epilogue: unit = (tile, 4 channels); Z[i][tile][co] f32x2 (48 KB) through LDS
   constexpr int CQ = 12, UNITS = Q_BT * CQ, UPT = (UNITS + 255) / 256;
-  constexpr bool RES = EPI & 1, RELU = EPI & 2;
   const float* res = reinterpret_cast<const float*>(p.res);
   float* yout = reinterpret_cast<float*>(p.y);
   size_t u_o[UPT];
@@ -301,7 +325,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     u_b[u] = (p.bias && live) ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int px = 0; px < 4; ++px)
-      u_r[u][px] = (RES && live) ? *reinterpret_cast<const f32x4*>(res + u_o[u] + (size_t)((px >> 1) * W + (px & 1)) * CO)
+      u_r[u][px] = (res && live) ? *reinterpret_cast<const f32x4*>(res + u_o[u] + (size_t)((px >> 1) * W + (px & 1)) * CO)
                                  : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   f32x2* zs = reinterpret_cast<f32x2*>(smem);
@@ -336,8 +360,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           const int h = c >> 1, e = (c & 1) * 2 + b2;
           const float y = a2 == 0 ? z[0][h][e] + z[1][h][e] + z[2][h][e] : z[1][h][e] - z[2][h][e] - z[3][h][e];
           float o = y + u_b[u][c];
-          if constexpr (RES) o += u_r[u][2 * a2 + b2][c];
-          if constexpr (RELU) o = fmaxf(o, 0.f);
+          if (res) o += u_r[u][2 * a2 + b2][c];
+          if (p.relu) o = fmaxf(o, 0.f);
           v[c] = o;
         }
         *reinterpret_cast<f32x4*>(yout + u_o[u] + (size_t)(a2 * W + b2) * CO) = v;
@@ -345,56 +369,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-template <int NCH, int PT, int EPI>
-hipError_t launch_qe(const ConvParams& p, hipStream_t s) {
-  constexpr int PPB = QPatch<PT>::PPB;
-  const int n_patches = p.N * p.To * (p.Ho / (2 * PT)) * (p.Wo / (2 * PT));
+template <int KO>
+hipError_t launch_probe(const ConvParams& p, hipStream_t s) {
+  constexpr int PPB = QPatch<4>::PPB;
+  const int n_patches = p.N * p.To * (p.Ho / 8) * (p.Wo / 8);
   const int n_co = p.Cout / 48;
-  hipLaunchKernelGGL((conv_wino_q<NCH, PT, EPI>), dim3(((n_patches + PPB - 1) / PPB) * n_co), dim3(256), 0, s, p, n_co,
+  hipLaunchKernelGGL((conv_wino_q_probe<8, 4, KO>), dim3(((n_patches + PPB - 1) / PPB) * n_co), dim3(256), 0, s, p, n_co,
                      n_patches);
   return hipGetLastError();
 }
-
-template <int NCH, int PT = 4>
-hipError_t launch_q(const ConvParams& p, hipStream_t s) {
-  switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
-    case 2: return launch_qe<NCH, PT, 2>(p, s);  // Conv2Plus1D spatial half: BN + ReLU, no residual
-    case 3: return launch_qe<NCH, PT, 3>(p, s);
-    case 1: return launch_qe<NCH, PT, 1>(p, s);
-    default: return launch_qe<NCH, PT, 0>(p, s);
-  }
-}
-
 }  // namespace
 
-bool winoq_supported(const ConvParams& p) {
-  return !p.in_bf16 && !p.out_bf16 && !p.stem && !p.x2 && p.KT == 1 && p.KH == 3 && p.KW == 3 && p.sh == 1 &&
-         p.sw == 1 && p.st == 1 && p.ph == 1 && p.pw == 1 && p.pt == 0 && p.Cin % 8 == 0 && p.Cout % 48 == 0 &&
-         p.Ho == p.Hi && p.Wo == p.Wi && p.To == p.Ti && p.Ho % 4 == 0 && p.Wo % 4 == 0 &&
-         (size_t)p.N * p.To * p.Ho * p.Wo * (p.Cin > p.Cout ? p.Cin : p.Cout) < ((size_t)1 << 31);
-}
-
-// p.w: conv_wino's U layout [Cin/8][4][Cout][4][4][2] (wino_transform_weights).
-hipError_t launch_winoq(const ConvParams& p, hipStream_t s) {
-  if (!winoq_supported(p)) return hipErrorInvalidValue;
-  if (p.Ho % 8 == 0 && p.Wo % 8 == 0) {  // 8x8-pixel patches
-    switch (p.Cin >> 3) {
-      case 8: return launch_q<8, 4>(p, s);
-      case 16: return launch_q<16, 4>(p, s);
-      default: return launch_q<0, 4>(p, s);
-    }
+// Knock-out probes of conv_wino_q (timing only; results are wrong for ko != 0): bit 1 no chunk
+// barrier, 2 no chunk vmcnt wait, 4 no transform, 8 no raw DMA, 16 no U loads, 32 no V operand reads.
+hipError_t launch_winoq_probe(const ConvParams& p, hipStream_t s, int ko) {
+  if (p.Cin != 64 || p.Ho % 8 || p.Wo % 8 || p.Cout % 48) return hipErrorInvalidValue;
+  switch (ko) {
+    case 0: return launch_probe<0>(p, s);
+    case 1: return launch_probe<1>(p, s);
+    case 2: return launch_probe<2>(p, s);
+    case 3: return launch_probe<3>(p, s);
+    case 4: return launch_probe<4>(p, s);
+    case 8: return launch_probe<8>(p, s);
+    case 12: return launch_probe<12>(p, s);
+    case 15: return launch_probe<15>(p, s);
+    case 16: return launch_probe<16>(p, s);
+    case 31: return launch_probe<31>(p, s);
+    case 63: return launch_probe<63>(p, s);
+    case 127: return launch_probe<127>(p, s);
+    case 191: return launch_probe<191>(p, s);
+    case 255: return launch_probe<255>(p, s);
+    case 64: return launch_probe<64>(p, s);
+    case 128: return launch_probe<128>(p, s);
+    case 256: return launch_probe<256>(p, s);
+    case 512: return launch_probe<512>(p, s);
   }
-  switch (p.Cin >> 3) {  // 4x4-pixel patches (28x28 maps)
-    case 8: return launch_q<8, 2>(p, s);
-    case 16: return launch_q<16, 2>(p, s);
-    default: return launch_q<0, 2>(p, s);
-  }
+  return hipErrorInvalidValue;
 }
-
-#ifdef CLASFV_KNOCKOUTS
-// tools/convbench.hip: the product dispatch
-hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko) {
-  (void)ko;
-  return launch_winoq(p, s);
-}
-#endif
