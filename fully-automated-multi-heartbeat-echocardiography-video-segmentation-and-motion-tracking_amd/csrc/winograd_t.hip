@@ -273,7 +273,8 @@ struct T5 {
   static_assert(NF * P * 2 % 64 == 0, "whole DMA instructions");
 };
 
-template <int TS, int NT>
+// EPI: epilogue form, bit 0 = residual add, bit 1 = ReLU (compile-time, no per-element selects).
+template <int TS, int NT, int EPI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_winot5(ConvParams p, int n_co,
                                                                                              int n_seg, int n_cols) {
   using G = T5<TS, NT>;
@@ -411,7 +412,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       f32x4 rv[4];
 #pragma unroll
       for (int a2 = 0; a2 < 4; ++a2)
-        rv[a2] = (res && ok) ? *reinterpret_cast<const f32x4*>(res + o + a2 * fstride) : f32x4{0.f, 0.f, 0.f, 0.f};
+        rv[a2] = ((EPI & 1) && ok) ? *reinterpret_cast<const f32x4*>(res + o + a2 * fstride) : f32x4{0.f, 0.f, 0.f, 0.f};
       const f32x4 m0 = acc[0][m][nt], m1 = acc[1][m][nt], m2 = acc[2][m][nt], m3 = acc[3][m][nt],
                   m4 = acc[4][m][nt], m5 = acc[5][m][nt];
       const f32x4 s12 = m1 + m2, d12 = m1 - m2, s34 = m3 + m4, d34 = m3 - m4;
@@ -423,8 +424,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if (ok) {
 #pragma unroll
         for (int a2 = 0; a2 < 4; ++a2) {
-          f32x4 vv = yv[a2] + bv + rv[a2];
-          if (p.relu) {
+          f32x4 vv = yv[a2] + bv;
+          if constexpr (EPI & 1) vv += rv[a2];
+          if constexpr (EPI & 2) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) vv[c] = fmaxf(vv[c], 0.f);
           }
@@ -435,12 +437,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-template <int TS, int NT>
-hipError_t winot5_launch(const ConvParams& p, hipStream_t s) {
+template <int TS, int NT, int EPI>
+hipError_t winot5_launch_e(const ConvParams& p, hipStream_t s) {
   using G = T5<TS, NT>;
   static bool attr = false;
   if (!attr && G::LDS > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_winot5<TS, NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_winot5<TS, NT, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        G::LDS);
     if (e != hipSuccess) return e;
     attr = true;
@@ -449,8 +451,18 @@ hipError_t winot5_launch(const ConvParams& p, hipStream_t s) {
   const int n_seg = (p.Ti / 4) / TS;
   const int n_co = p.Cout / G::CB;
   const int nb = ((n_cols + G::P - 1) / G::P) * n_seg * n_co;
-  hipLaunchKernelGGL((conv_winot5<TS, NT>), dim3(nb), dim3(256), G::LDS, s, p, n_co, n_seg, n_cols);
+  hipLaunchKernelGGL((conv_winot5<TS, NT, EPI>), dim3(nb), dim3(256), G::LDS, s, p, n_co, n_seg, n_cols);
   return hipGetLastError();
+}
+
+template <int TS, int NT>
+hipError_t winot5_launch(const ConvParams& p, hipStream_t s) {
+  switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
+    case 2: return winot5_launch_e<TS, NT, 2>(p, s);  // TP1 / stem T: BN + ReLU
+    case 3: return winot5_launch_e<TS, NT, 3>(p, s);  // TP2: BN + residual + ReLU
+    case 1: return winot5_launch_e<TS, NT, 1>(p, s);
+    default: return winot5_launch_e<TS, NT, 0>(p, s);
+  }
 }
 
 // 64 channels per wave (NT = 4); 32 when that leaves fewer than two blocks per CU (layer3 maps).
