@@ -24,6 +24,11 @@ struct ConvParams {
   int Cin2;
   int stem;           // fp32 4-channel input (3 + pad): register-staged kernel, per-float4 tap decode
   int in_bf16, out_bf16;
+  // 8-channel-blocked activations [C/8][N*T*H*W][8] instead of channels-last (fp32 only): the
+  // mid tensor of a Conv2Plus1D between a stride-1 spatial producer (conv_wino_q on 8x8-pixel
+  // patches and conv_stem_f32 write y_c8) and the temporal Winograd consumer (conv_winot5 reads x_c8), whose
+  // 8-channel chunks then read whole 128-B lines instead of 32 B of every pixel.
+  int x_c8, y_c8;
 };
 
 // Decoder tap: low-resolution projection P_i = (s1 * W_i) . f_i, channels-last with 64 channels.
@@ -66,6 +71,8 @@ void winor_transform_weights(const double* w, int cout, int cin, int cout_p, int
 // Fused Winograd F(4,3)-in-time path for stride-1 3x1x1 fp32 convs; p.w = transformed weights.
 bool winot_supported(const ConvParams& p);
 hipError_t launch_winot(const ConvParams& p, hipStream_t s);
+// launch_winot would run conv_winot5, the variant that also reads 8-channel-blocked input (x_c8).
+bool winot_c8_ok(const ConvParams& p);
 // U[cin_p/8][6][cout_p/64][64][8] from folded weights w[cout][cin][3] (double).
 void winot_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 // Patch-staged bf16 implicit GEMM for stride-1 1x3x3 and 3x1x1 convs (conv_patch.hip); p.w = conv_dma's

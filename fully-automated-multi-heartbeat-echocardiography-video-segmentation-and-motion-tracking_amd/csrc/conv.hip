@@ -66,7 +66,8 @@ __device__ inline void epilogue(const ConvParams& p, const f32x4 (&acc)[MT][NT],
     for (int j = 0; j < NT; ++j) {
       const int n = n0 + j * 16 + 4 * q;
       if (n >= p.Cout) continue;
-      const size_t o = (size_t)m * p.Cout + n;
+      // channels-last, or 8-channel blocks [Cout/8][M][8] (p.y_c8, fp32)
+      const size_t o = p.y_c8 ? ((size_t)(n >> 3) * p.M + m) * 8 + (n & 7) : (size_t)m * p.Cout + n;
       const f32x4 bv = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
       const f32x4 rv = p.res ? load_res4(p.res, o, p.out_bf16) : f32x4{0.f, 0.f, 0.f, 0.f};
       f32x4 v = acc[i][j] + bv + rv;
@@ -138,15 +139,29 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles) {
   const int khw = p.KH * p.KW;
   const int kmain = p.KT * khw * p.Cin;  // K columns from x; the rest (1x1 dual input) from x2
 
+  // K-step cursor (issue() is called for k_step = 0, 1, 2, ... in order): channel offset c0 inside
+  // tap (kt, kh, kw) of input x, then of x2 -- advanced incrementally, where the per-step scalar
+  // divisions of the closed form cost ~3 SALU instructions per MFMA (PMC, layer2 SP1)
+  int c_c0 = 0, c_kt = 0, c_kh = 0, c_kw = 0, c_tap_pix = 0;
+  bool c_second = kmain == 0;
   auto issue = [&](int k_step, int slot) {
     const int k0 = k_step * BKE;
-    const bool second = k0 >= kmain;
+    const bool second = c_second;
     const int cin = second ? p.Cin2 : p.Cin;
     const T* xb = second ? x2 : x;
-    const int kk0 = second ? k0 - kmain : k0;
-    const int tap = kk0 / cin, c0 = kk0 - tap * cin;
-    const int kt = tap / khw, rem = tap - kt * khw, kh = rem / p.KW, kw = rem - kh * p.KW;
-    const int tap_pix = (kt * p.Hi + kh) * p.Wi + kw;
+    const int c0 = c_c0, kt = c_kt, kh = c_kh, kw = c_kw, tap_pix = c_tap_pix;
+    c_c0 += BKE;
+    if (c_c0 == cin) {
+      c_c0 = 0;
+      if (++c_kw == p.KW) {
+        c_kw = 0;
+        if (++c_kh == p.KH) {
+          c_kh = 0;
+          if (++c_kt == p.KT) c_kt = 0, c_second = true;
+        }
+      }
+      c_tap_pix = (c_kt * p.Hi + c_kh) * p.Wi + c_kw;
+    }
     const T* xc = xb + c0 + EPS * dq;
 #pragma unroll
     for (int j = 0; j < PER_WAVE; ++j) {

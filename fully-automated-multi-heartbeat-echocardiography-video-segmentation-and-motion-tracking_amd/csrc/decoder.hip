@@ -163,7 +163,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
   extern __shared__ __align__(16) float smem[];
   float* stage = smem;  // STAGE_FLOATS
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // voxel-row loops below are scalar branches
   const int q = lane >> 4, l16 = lane & 15;
   const int tiles_w = p.W / TILE_W, tiles = (p.H / TILE_H) * tiles_w;
   // 1-D grid, XCD-aware: consecutive logical tiles (row-major in a frame, then frame, then clip) land
@@ -253,45 +254,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
   const size_t TH = (size_t)p.T * HW;
   // Both voxel rows of the wave are interpolated first, then share every W2 fragment load (W2 is
   // re-read from L1/L2 once per wave rather than once per row: the loads were the kernel's fixed cost).
+  // Separable form, W then H (PyTorch's nesting): the wave's two voxel rows hr, hr + 1 (every tap
+  // upsamples by more than 2, so they touch at most 3 consecutive source rows, wave-uniformly) share
+  // each source row's column interpolation hx = lx0 P[r][x0] + lx1 P[r][x1]: 8 LDS reads per source
+  // row, 16-24 per tap for both rows instead of 32.
   f32x4 h1[2][4];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int hr = h0 + 2 * wid + mt;
+  for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int c = 0; c < 4; ++c) h1[mt][c] = *reinterpret_cast<const f32x4*>(p.b1 + 16 * c + 4 * q);
+  const int hr = h0 + 2 * wid;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const DecTap& tp = p.tap[i];
-      const Win& w = win[i];
-      int x0, x1, y0, y1;
-      float lx0, lx1, ly0, ly1;
-      src_index(tp.sw, w0 + l16, tp.W, x0, x1, lx0, lx1);
-      src_index(tp.sh, hr, tp.H, y0, y1, ly0, ly1);
-      x0 -= w.c0;
-      x1 -= w.c0;
-      y0 -= w.r0;
-      y1 -= w.r0;
-      const float* fb = stage + kPixOff[i] * PIX + 4 * q;
-      const float* p00 = fb + (y0 * w.nc + x0) * PIX;
-      const float* p01 = fb + (y0 * w.nc + x1) * PIX;
-      const float* p10 = fb + (y1 * w.nc + x0) * PIX;
-      const float* p11 = fb + (y1 * w.nc + x1) * PIX;
-      const float w00 = ly0 * lx0, w01 = ly0 * lx1, w10 = ly1 * lx0, w11 = ly1 * lx1;
+  for (int i = 0; i < 4; ++i) {
+    const DecTap& tp = p.tap[i];
+    const Win& w = win[i];
+    int x0, x1, ya0, ya1, yb0, yb1;
+    float lx0, lx1, la0, la1, lb0, lb1;
+    src_index(tp.sw, w0 + l16, tp.W, x0, x1, lx0, lx1);
+    src_index(tp.sh, hr, tp.H, ya0, ya1, la0, la1);
+    src_index(tp.sh, hr + 1, tp.H, yb0, yb1, lb0, lb1);
+    const int nrows = yb1 - ya0 + 1;  // 1..3, wave-uniform
+    const float* fb = stage + kPixOff[i] * PIX + 4 * q + (ya0 - w.r0) * w.nc * PIX;
+    const float* c0p = fb + (x0 - w.c0) * PIX;
+    const float* c1p = fb + (x1 - w.c0) * PIX;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (k >= nrows) break;
+      // weights of source row ya0 + k in output rows hr (wa) and hr + 1 (wb)
+      const float wa = (k == 0 ? la0 : 0.f) + (ya1 - ya0 == k ? la1 : 0.f);
+      const float wb = (yb0 - ya0 == k ? lb0 : 0.f) + (yb1 - ya0 == k ? lb1 : 0.f);
+      const int ro = k * w.nc * PIX;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        h1[mt][c] += *reinterpret_cast<const f32x4*>(p00 + 16 * c) * w00;
-        h1[mt][c] += *reinterpret_cast<const f32x4*>(p01 + 16 * c) * w01;
-        h1[mt][c] += *reinterpret_cast<const f32x4*>(p10 + 16 * c) * w10;
-        h1[mt][c] += *reinterpret_cast<const f32x4*>(p11 + 16 * c) * w11;
+        const f32x4 hx = *reinterpret_cast<const f32x4*>(c0p + ro + 16 * c) * lx0 +
+                         *reinterpret_cast<const f32x4*>(c1p + ro + 16 * c) * lx1;
+        h1[0][c] += hx * wa;
+        h1[1][c] += hx * wb;
       }
-      // one tap's 16 LDS reads in flight at a time (hoisting all four taps' reads spills)
+      // one source row's 8 LDS reads in flight at a time (hoisting more spills)
       __builtin_amdgcn_sched_barrier(0);
     }
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int j = 0; j < 4; ++j) h1[mt][c][j] = fmaxf(h1[mt][c][j], 0.f);
-  }
 
   if constexpr (BF) {
     decoder_heads_bf16(p, h1, t, n, h0, w0, wid, q, l16);

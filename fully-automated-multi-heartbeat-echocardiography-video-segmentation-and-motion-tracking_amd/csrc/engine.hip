@@ -316,86 +316,109 @@ double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
   return 2.0 * (ceil(m / 128.0) * 128.0) * c.cout_p * (double)c.Kp * 1e-9;
 }
 
-int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
-             hipStream_t s, const void* zero_block, const void* x2, const char** kname) {
+// Conv parameters of c over an input of shape `in` (output shape in `out`; tensors unset).
+ConvParams conv_params(const Conv& c, const Shape5& in, Shape5& out) {
   out.n = in.n;
   out.t = (in.t + 2 * c.pt - c.kt) / c.st + 1;
   out.h = (in.h + 2 * c.ph - c.kh) / c.sh + 1;
   out.w = (in.w + 2 * c.pw - c.kw) / c.sw + 1;
   out.c = c.cout_p;
-  if (in.c != c.cin_p) return fail(CLASFV_EINVAL, "internal: channel mismatch");
   ConvParams p{};
-  p.x = x;
   p.w = c.dw;
   p.bias = c.db;
-  p.res = res;
-  p.y = y;
   p.N = in.n, p.Ti = in.t, p.Hi = in.h, p.Wi = in.w, p.Cin = in.c;
   p.To = out.t, p.Ho = out.h, p.Wo = out.w, p.Cout = out.c;
   p.KT = c.kt, p.KH = c.kh, p.KW = c.kw, p.st = c.st, p.sh = c.sh, p.sw = c.sw, p.pt = c.pt, p.ph = c.ph, p.pw = c.pw;
   p.K = c.K, p.Kp = c.Kp;
   p.M = out.n * out.t * out.h * out.w;
-  p.relu = relu ? 1 : 0;
-  p.zero = zero_block;
-  p.x2 = x2;
   p.Cin2 = c.cin2;
   p.stem = c.stem;
   p.in_bf16 = c.in_bf16;
   p.out_bf16 = c.out_bf16;
+  return p;
+}
+
+// The kernel run_conv launches for c with parameters p (the A/B switches are read here).
+const char* pick_kernel(const Conv& c, ConvParams p) {
   // F(2x4,3x3) is opt-in: 25 % fewer MFMAs than conv_wino_q but 1.5x its U operand traffic per
   // output; measured slower on layer1 (2.80 vs 2.40 ms)
-  if (c.dwinor && getenv("CLASFV_WINO_R") && winor_supported(p)) {
-    p.w = c.dwinor;
-    HIP_TRY(launch_winor(p, s));
-    *kname = "conv_wino_r";
-    return CLASFV_OK;
-  }
+  if (c.dwinor && getenv("CLASFV_WINO_R") && winor_supported(p)) return "conv_wino_r";
   if (c.dwino) {
-    p.w = c.dwino;
     const bool no_patch = getenv("CLASFV_NO_WINO_PATCH") != nullptr;  // A/B switch (tests)
-    if (!no_patch && winoq_supported(p)) {
-      HIP_TRY(launch_winoq(p, s));
-      *kname = "conv_wino_q";
-      return CLASFV_OK;
-    }
-    if (wino_supported(p)) {
-      HIP_TRY(launch_wino(p, s));
-      *kname = "conv_wino";
-      return CLASFV_OK;
-    }
-    p.w = c.dw;
+    if (!no_patch && winoq_supported(p)) return "conv_wino_q";
+    if (wino_supported(p)) return "conv_wino";
   }
   static const bool no_stem_bf16 = getenv("CLASFV_NO_STEM_BF16") != nullptr;  // A/B switch (tests)
-  if (c.dws16 && !no_stem_bf16 && stem_bf16_supported(p)) {
+  if (c.dws16 && !no_stem_bf16 && stem_bf16_supported(p)) return "conv_stem_bf16";
+  if (c.dwinot && winot_supported(p)) return "conv_winot";
+  const bool no_patch_bf16 = getenv("CLASFV_NO_PATCH_BF16") != nullptr;  // A/B switch (tests)
+  if (!no_patch_bf16 && patch_bf16_supported(p)) return "conv_patch_bf16";
+  return c.stem ? "conv_stem_f32" : "conv_dma";
+}
+
+// Whether the mid tensor between producer `a` (input shape `in`) and consumer `b` goes through HBM
+// in the 8-channel-blocked layout: `a` runs on a kernel that writes it and `b` on conv_winot5,
+// which reads it (CLASFV_NO_C8=1: always channels-last, A/B switch).
+bool c8_pair(const Conv& a, const Conv& b, const Shape5& in) {
+  if (getenv("CLASFV_NO_C8")) return false;
+  Shape5 mid, out;
+  ConvParams pa = conv_params(a, in, mid);
+  ConvParams pb = conv_params(b, mid, out);
+  pa.w = a.dwino ? (const void*)a.dwino : a.dw;
+  pb.w = b.dwinot;
+  const char* ka = pick_kernel(a, pa);
+  // Measured per producer (30 clips, profiles/r02j_*): stem and conv_wino_q on 8x8-pixel patches
+  // (layer1) write the blocked layout at no cost while the temporal kernels after them gain 17-24 %;
+  // conv_wino_q on 4x4-pixel patches (layer2, 28x28 maps) lost 12 % to its scattered 32-B pieces
+  // for a 7 % gain downstream, conv_wino (layer3) broke even: those stay channels-last.
+  const bool writes = (!strcmp(ka, "conv_wino_q") && pa.Ho % 8 == 0 && pa.Wo % 8 == 0) || !strcmp(ka, "conv_stem_f32");
+  return writes && !a.out_bf16 && !strcmp(pick_kernel(b, pb), "conv_winot") && winot_c8_ok(pb);
+}
+
+int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
+             hipStream_t s, const void* zero_block, const void* x2, const char** kname, int x_c8 = 0, int y_c8 = 0) {
+  if (in.c != c.cin_p) return fail(CLASFV_EINVAL, "internal: channel mismatch");
+  ConvParams p = conv_params(c, in, out);
+  p.x = x;
+  p.res = res;
+  p.y = y;
+  p.relu = relu ? 1 : 0;
+  p.zero = zero_block;
+  p.x2 = x2;
+  p.x_c8 = x_c8;
+  p.y_c8 = y_c8;
+  const char* k = pick_kernel(c, p);
+  *kname = k;
+  const bool c8_out = !strcmp(k, "conv_wino_q") || !strcmp(k, "conv_stem_f32");
+  if ((y_c8 && !c8_out) || (x_c8 && strcmp(k, "conv_winot")))
+    return fail(CLASFV_EINVAL, "internal: 8-channel-blocked layout on an unsupported kernel");
+  if (!strcmp(k, "conv_wino_r")) {
+    p.w = c.dwinor;
+    HIP_TRY(launch_winor(p, s));
+  } else if (!strcmp(k, "conv_wino_q")) {
+    p.w = c.dwino;
+    HIP_TRY(launch_winoq(p, s));
+  } else if (!strcmp(k, "conv_wino")) {
+    p.w = c.dwino;
+    HIP_TRY(launch_wino(p, s));
+  } else if (!strcmp(k, "conv_stem_bf16")) {
     p.w = c.dws16;
     HIP_TRY(launch_stem_bf16(p, s));
-    *kname = "conv_stem_bf16";
-    return CLASFV_OK;
-  }
-  if (c.dwinot) {
+  } else if (!strcmp(k, "conv_winot")) {
     p.w = c.dwinot;
-    if (winot_supported(p)) {
-      HIP_TRY(launch_winot(p, s));
-      *kname = "conv_winot";
-      return CLASFV_OK;
-    }
-    p.w = c.dw;
-  }
-  const bool no_patch_bf16 = getenv("CLASFV_NO_PATCH_BF16") != nullptr;  // A/B switch (tests)
-  if (!no_patch_bf16 && patch_bf16_supported(p)) {
+    HIP_TRY(launch_winot(p, s));
+  } else if (!strcmp(k, "conv_patch_bf16")) {
     HIP_TRY(launch_patch_bf16(p, s));
-    *kname = "conv_patch_bf16";
-    return CLASFV_OK;
+  } else {
+    int mt = 2, bn = c.cout_p;  // stem: one N tile (48 fp32 / 64 bf16 channels)
+    if (!c.stem) {
+      static const int force_nt = getenv("CLASFV_CONV_NT") ? atoi(getenv("CLASFV_CONV_NT")) : 0;
+      conv_pick_tile(p.M, c.cout_p, force_nt, &mt, &bn);
+      static const int force_mt = getenv("CLASFV_CONV_MT") ? atoi(getenv("CLASFV_CONV_MT")) : 0;
+      if (force_mt == 4 && p.in_bf16) mt = 4;  // A/B switch
+    }
+    HIP_TRY(launch_conv(p, mt, bn, s));
   }
-  int mt = 2, bn = c.cout_p;  // stem: one N tile (48 fp32 / 64 bf16 channels)
-  if (!c.stem) {
-    static const int force_nt = getenv("CLASFV_CONV_NT") ? atoi(getenv("CLASFV_CONV_NT")) : 0;
-    conv_pick_tile(p.M, c.cout_p, force_nt, &mt, &bn);
-    static const int force_mt = getenv("CLASFV_CONV_MT") ? atoi(getenv("CLASFV_CONV_MT")) : 0;
-    if (force_mt == 4 && p.in_bf16) mt = 4;  // A/B switch
-  }
-  HIP_TRY(launch_conv(p, mt, bn, s));
-  *kname = c.stem ? "conv_stem_f32" : "conv_dma";
   return CLASFV_OK;
 }
 
@@ -716,9 +739,9 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
     last_ev = e;
   };
   auto run = [&](const Conv& c, const void* xin, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
-                 const void* x2 = nullptr) {
+                 const void* x2 = nullptr, int x_c8 = 0, int y_c8 = 0) {
     const char* kname = "";
-    int rc_ = run_conv(c, xin, in, y, out, res, relu, s, h->zero, x2, &kname);
+    int rc_ = run_conv(c, xin, in, y, out, res, relu, s, h->zero, x2, &kname, x_c8, y_c8);
     if (!rc_) timed(kname, conv_gflop(c, out), conv_exec_gflop(c, out, kname));
     return rc_;
   };
@@ -728,8 +751,10 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   Shape5 sx{N, T, H, W, 4}, s0, sx0;
   int rc;
   size_t ci = 0;
-  if ((rc = run(h->convs[ci++], buf(XIN), sx, buf(S0), s0, nullptr, true))) return rc;
-  if ((rc = run(h->convs[ci++], buf(S0), s0, buf(X0), sx0, nullptr, true))) return rc;
+  // Conv2Plus1D mid tensors (and the stem's) are 8-channel-blocked where c8_pair allows
+  const int c8s = c8_pair(h->convs[0], h->convs[1], sx);
+  if ((rc = run(h->convs[ci++], buf(XIN), sx, buf(S0), s0, nullptr, true, nullptr, 0, c8s))) return rc;
+  if ((rc = run(h->convs[ci++], buf(S0), s0, buf(X0), sx0, nullptr, true, nullptr, c8s, 0))) return rc;
   const int outs[4][2] = {{L1A, L1}, {L2A, L2}, {L3A, L3}, {L4A, L4}};
   void* cur = buf(X0);
   Shape5 cs = sx0, taps_shape[5];
@@ -744,16 +769,18 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
       const Conv& tp2 = h->convs[ci++];
       const Conv* ds = (ci < h->convs.size() && h->convs[ci].role == DS) ? &h->convs[ci++] : nullptr;
       Shape5 sm, sa, sm2, so, sd;
-      if ((rc = run(sp1, cur, cs, buf(MID), sm, nullptr, true))) return rc;
-      if ((rc = run(tp1, buf(MID), sm, buf(TA), sa, nullptr, true))) return rc;
-      if ((rc = run(sp2, buf(TA), sa, buf(MID), sm2, nullptr, true))) return rc;
+      const int c8a = c8_pair(sp1, tp1, cs);
+      if ((rc = run(sp1, cur, cs, buf(MID), sm, nullptr, true, nullptr, 0, c8a))) return rc;
+      if ((rc = run(tp1, buf(MID), sm, buf(TA), sa, nullptr, true, nullptr, c8a, 0))) return rc;
+      const int c8b = c8_pair(sp2, tp2, sa);
+      if ((rc = run(sp2, buf(TA), sa, buf(MID), sm2, nullptr, true, nullptr, 0, c8b))) return rc;
       const void* res = cur;
       if (ds) {
         if ((rc = run(*ds, cur, cs, buf(DSB), sd, nullptr, false))) return rc;
         res = buf(DSB);
       }
       void* out = buf(outs[li][b]);
-      if ((rc = run(tp2, buf(MID), sm2, out, so, res, true))) return rc;
+      if ((rc = run(tp2, buf(MID), sm2, out, so, res, true, nullptr, c8b, 0))) return rc;
       cur = out;
       cs = so;
     }

@@ -66,7 +66,7 @@ static_assert(QPatch<2>::DPW == 3 && QPatch<2>::LDS <= 80 * 1024, "PT = 2 layout
 
 // EPI: epilogue form, bit 0 = residual add, bit 1 = ReLU (compile-time: as runtime flags every
 // output element carried two selects).
-template <int NCH, int PT = 4, int EPI = 2>
+template <int NCH, int PT = 4, int EPI = 2, bool C8 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino_q(ConvParams p, int n_co,
                                                                                              int n_patches) {
   using G = QPatch<PT>;
@@ -281,6 +281,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   constexpr bool RES = EPI & 1, RELU = EPI & 2;
   const float* res = reinterpret_cast<const float*>(p.res);
   float* yout = reinterpret_cast<float*>(p.y);
+  // output pixel stride: channels-last, or 8-channel blocks [CO/8][pixels][8] (C8 = p.y_c8; a
+  // compile-time form: as a runtime flag the PT = 2 instances spilled)
+  const int ps = C8 ? 8 : CO;
+  const size_t plane = (size_t)n_patches * (4 * PT * PT) * 8;
   size_t u_o[UPT];
   int u_ok[UPT], u_z[UPT];
   f32x4 u_b[UPT], u_r[UPT][4];
@@ -295,13 +299,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int pr = r / PX, pc = r - pr * PX;
     const int yy = pr * 2 * PT + 2 * ((tl / PT) % PT), xx = pc * 2 * PT + 2 * (tl % PT);
     const int co = n0 + 4 * cq;
-    u_o[u] = ((size_t)(f * H + yy) * W + xx) * CO + co;
+    const size_t pix = (size_t)(f * H + yy) * W + xx;
+    u_o[u] = C8 ? (co >> 3) * plane + pix * 8 + (co & 7) : pix * CO + co;
     u_z[u] = tl * 48 + 4 * cq;
     u_ok[u] = live;
     u_b[u] = (p.bias && live) ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int px = 0; px < 4; ++px)
-      u_r[u][px] = (RES && live) ? *reinterpret_cast<const f32x4*>(res + u_o[u] + (size_t)((px >> 1) * W + (px & 1)) * CO)
+      u_r[u][px] = (RES && live) ? *reinterpret_cast<const f32x4*>(res + u_o[u] + (size_t)((px >> 1) * W + (px & 1)) * ps)
                                  : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   f32x2* zs = reinterpret_cast<f32x2*>(smem);
@@ -340,7 +345,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           if constexpr (RELU) o = fmaxf(o, 0.f);
           v[c] = o;
         }
-        *reinterpret_cast<f32x4*>(yout + u_o[u] + (size_t)(a2 * W + b2) * CO) = v;
+        *reinterpret_cast<f32x4*>(yout + u_o[u] + (size_t)(a2 * W + b2) * ps) = v;
       }
   }
 }
@@ -350,8 +355,16 @@ hipError_t launch_qe(const ConvParams& p, hipStream_t s) {
   constexpr int PPB = QPatch<PT>::PPB;
   const int n_patches = p.N * p.To * (p.Ho / (2 * PT)) * (p.Wo / (2 * PT));
   const int n_co = p.Cout / 48;
-  hipLaunchKernelGGL((conv_wino_q<NCH, PT, EPI>), dim3(((n_patches + PPB - 1) / PPB) * n_co), dim3(256), 0, s, p, n_co,
-                     n_patches);
+  const dim3 grid(((n_patches + PPB - 1) / PPB) * n_co);
+  if constexpr (PT == 4) {  // 8-channel-blocked output: 8x8-pixel patches only (engine.hip, c8_pair)
+    if (p.y_c8) {
+      hipLaunchKernelGGL((conv_wino_q<NCH, PT, EPI, true>), grid, dim3(256), 0, s, p, n_co, n_patches);
+      return hipGetLastError();
+    }
+  } else {
+    if (p.y_c8) return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL((conv_wino_q<NCH, PT, EPI, false>), grid, dim3(256), 0, s, p, n_co, n_patches);
   return hipGetLastError();
 }
 

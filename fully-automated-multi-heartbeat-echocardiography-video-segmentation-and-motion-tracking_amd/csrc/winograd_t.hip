@@ -291,6 +291,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int T = p.To, HW = p.Ho * p.Wo, C = p.Cin, CO = p.Cout;
   const int t_seg = seg * 4 * TS;
   const int nchunk = C >> 3;
+  // input pixel stride and chunk stride (floats): channels-last, or 8-channel blocks (x_c8)
+  const int cs = p.x_c8 ? 8 : C;
+  const size_t kstride = p.x_c8 ? (size_t)p.N * T * HW * 8 : 8;
   constexpr int DMAX = (G::NI + 3) / 4;           // DMA instructions of waves 0 .. (NI % 4) - 1
   constexpr int DMIN = G::NI / 4;                 // ... of the others
   const bool more = (G::NI % 4 == 0) || wid < G::NI % 4;
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       gc = gc < n_cols ? gc : n_cols - 1;
       t = t < 0 ? 0 : (t >= T ? T - 1 : t);
       const int n = gc / HW, pix = gc - n * HW;
-      off = (unsigned)(((n * T + t) * HW + pix) * C + half * 4) * 4u;
+      off = (unsigned)(((n * T + t) * HW + pix) * cs + half * 4) * 4u;
     } else if (I < G::NI) {
       const int s = (I - G::RAW_I) * 64 + lane;  // (e, co, stored half)
       const int e = s / (2 * G::CB), co = (s >> 1) % G::CB, half = (s & 1) ^ ((co >> 3) & 1);
@@ -319,7 +322,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     d_off[j] = off;
   }
   auto issue = [&](int k, int stage) __attribute__((always_inline)) {
-    const char* xk = reinterpret_cast<const char*>(x + k * 8);
+    const char* xk = reinterpret_cast<const char*>(x + k * kstride);
     const char* uk = reinterpret_cast<const char*>(U + (size_t)k * 6 * CO * 8);
 #pragma unroll
     for (int j = 0; j < DMAX; ++j) {
@@ -480,6 +483,10 @@ bool winot5_fits(const ConvParams& p) { return (size_t)p.N * p.Ti * p.Hi * p.Wi 
 
 }  // namespace
 
+bool winot_c8_ok(const ConvParams& p) {
+  return winot_supported(p) && getenv("CLASFV_WINOT_REFERENCE") == nullptr && p.Ti % 8 == 0 && winot5_fits(p);
+}
+
 bool winot_supported(const ConvParams& p) {
   return !p.in_bf16 && !p.out_bf16 && !p.stem && !p.x2 && p.KT == 3 && p.KH == 1 && p.KW == 1 && p.st == 1 &&
          p.sh == 1 && p.sw == 1 && p.pt == 1 && p.ph == 0 && p.pw == 0 && p.Cin % 8 == 0 && p.Cout % BN == 0 &&
@@ -493,8 +500,8 @@ hipError_t launch_winot(const ConvParams& p, hipStream_t s) {
   // CLASFV_WINOT_REFERENCE=1 (tests): always conv_winot; both kernels compute the same products in
   // the same order (bit-identical outputs). conv_winot5 needs T % 8 == 0 (whole tile pairs);
   // layer4 at 32-frame clips (T = 4, fewer than 256 blocks) stays on conv_winot.
-  const bool reference = getenv("CLASFV_WINOT_REFERENCE") != nullptr;
-  if (!reference && p.Ti % 8 == 0 && winot5_fits(p)) return winot5_dispatch(p, s);
+  if (winot_c8_ok(p)) return winot5_dispatch(p, s);
+  if (p.x_c8) return hipErrorInvalidValue;  // 8-channel-blocked input: conv_winot5 only
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)conv_winot, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -512,6 +519,7 @@ hipError_t launch_winot(const ConvParams& p, hipStream_t s) {
 // tools/convbench.hip: run one temporal kernel variant (0 conv_winot, 500 conv_winot5); timing and
 // bit-identity comparisons only, not product code.
 hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko) {
+  if (p.x_c8 && ko == 0) return hipErrorInvalidValue;
   switch (ko) {
     case 0: {
       hipError_t e = hipFuncSetAttribute((const void*)conv_winot, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -521,7 +529,7 @@ hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko) {
                          p.Cout / BN, n_tiles);
       return hipGetLastError();
     }
-    case 500: return winot5_dispatch(p, s);
+    case 500: return p.x_c8 && !winot_c8_ok(p) ? hipErrorInvalidValue : winot5_dispatch(p, s);
     case 502: return winot5_dispatch(p, s, 2);
     case 504: return winot5_dispatch(p, s, 4);
   }

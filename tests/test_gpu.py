@@ -563,6 +563,20 @@ def test_kernel_variants_bitexact(model, monkeypatch, shape):
     assert torch.equal(s_new, s_old) and torch.equal(m_new, m_old)
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (1, 3, 8, 32, 48)])
+def test_c8_blocked_mid_bitexact(model, monkeypatch, shape):
+    """The 8-channel-blocked mid tensors (stem and Conv2Plus1D spatial -> temporal Winograd) only
+    change where values live in HBM: the forward is bit-identical to the channels-last one
+    (CLASFV_NO_C8=1)."""
+    rng = np.random.default_rng(31)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    s_b, m_b = model(x)
+    monkeypatch.setenv("CLASFV_NO_C8", "1")
+    s_c, m_c = model(x)
+    monkeypatch.delenv("CLASFV_NO_C8")
+    assert torch.equal(s_b, s_c) and torch.equal(m_b, m_c)
+
+
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112)])
 def test_wino_f2x4_matches_f2x2(model, monkeypatch, shape):
     """conv_wino_r (F(2x4,3x3), opt-in with CLASFV_WINO_R where H, W % 8 == 0) against conv_wino_q
