@@ -54,7 +54,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, l16 = lane & 15;
   const int blk = xcd_swizzle_w(blockIdx.x, gridDim.x);
-  const int t0 = (blk / n_co) * BT, n0 = (blk % n_co) * 16 * NT;
+  // Block order (one XCD runs a contiguous range of it): groups of G co blocks outermost, then tile
+  // blocks, then the G co blocks of the group -- an XCD's co-resident blocks then need the U slices of
+  // G co blocks (<= 3 MB at layer3/4 widths, L2-resident) instead of all n_co (9.4 / 38 MB, which
+  // every tile block re-streamed from the fabric: FETCH 27x the algorithmic bytes).
+  const int G = n_co % 4 == 0 ? 4 : n_co % 3 == 0 ? 3 : n_co % 2 == 0 ? 2 : 1;
+  const int n_tb = (n_tiles + BT - 1) / BT;
+  const int grp = blk / (n_tb * G), grem = blk - grp * (n_tb * G);
+  const int t0 = (grem / G) * BT, n0 = (grp * G + grem % G) * 16 * NT;
   const int H = p.Ho, W = p.Wo, C = p.Cin, CO = p.Cout;
   const int TY = (H + 1) >> 1, TX = (W + 1) >> 1;
   const int nchunk = NCH > 0 ? NCH : C >> 3;
