@@ -46,11 +46,9 @@ template <int PT>
 struct QPatch {
   static constexpr int SIDE = 2 * PT + 2;                 // input patch side (pixels)
   static constexpr int PIX = SIDE * SIDE;
-  // pixels between the patches of a raw stage. PT = 4: 101 (one pad pixel), so that the transform's
-  // wave (one tile row ly of both patches: 4 lx x 2 patches x 8 channels) reads pixels whose 32-B
-  // slots fall in 8 distinct bank groups: 2 lx + 5 pp (mod 8). At a 100-pixel stride every
-  // transform ds_read_b32 and V write was 2-way bank-conflicted.
-  static constexpr int PSTRIDE = PT == 4 ? PIX + 1 : PIX;
+  // pixels between the patches of a raw stage: odd (one pad pixel), so that two patches' pixels of
+  // one transform read fall on different 32-B bank quads (see tt below).
+  static constexpr int PSTRIDE = PIX + 1;
   static constexpr int PPB = Q_BT / (PT * PT);            // patches per block
   static constexpr int SLOTS = PPB * PSTRIDE * 2;         // 16-B DMA slots per chunk (8 channels)
   static constexpr int DPW = ((SLOTS + 63) / 64 + 3) / 4;  // DMAs per wave per chunk
@@ -124,10 +122,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int h = 0; h < 2; ++h) u[nt][h] = *reinterpret_cast<const f32x4*>(b + (size_t)nt * 16 * 32 + h * 4);
   };
   // transform thread = (tile tt = pp*PT*PT + ly*PT + lx, channel cc)
-  // (PT = 4: wave = tile row ly of both patches, lane = (patch, lx, channel); PT = 2: 8 consecutive tiles)
-  const int tt = PT == 4 ? (lane >> 5) * 16 + wid * 4 + ((lane >> 3) & 3) : tid >> 3, cc = tid & 7;
+  // (PT = 2: 8 consecutive tiles per wave; PT = 4: wave = tile row ly of both patches, lane = (lx bit 1, patch, lx bit 0, channel): the
+  // ds_read_b32 32-lane groups then hold lx in {0,1} or {2,3} x both patches, whose 32-B slots --
+  // 16 lx + 8 pp (mod 32, PSTRIDE = 101) -- cover all 32 banks; lane = (patch, lx, channel) put
+  // lx = 0 / 2 and 1 / 3 on the same banks, 2-way)
+  // PT = 2: wave = patches 2 wid, 2 wid + 1, lane = (ly, patch bit, lx, channel): a 32-lane group is
+  // lx x 2 patches, slots 2 lx + 37 pp (mod 4) all distinct (lane = (patch, ly, lx, channel) put ly = 0
+  // and 1 on the same banks)
+  const int tt = PT == 4 ? ((lane >> 4) & 1) * 16 + wid * 4 + ((lane >> 3) & 1) + 2 * (lane >> 5)
+                         : (2 * wid + ((lane >> 4) & 1)) * 4 + (lane >> 5) * 2 + ((lane >> 3) & 1);
+  const int cc = tid & 7;
   const int raw_off = (tt / (PT * PT)) * G::PSTRIDE * 8 + (2 * ((tt / PT) % PT) * G::SIDE + 2 * (tt % PT)) * 8 + cc;
-  const int v_off = (((tt & 15) * 4 + (cc >> 1)) * 2 + (tt >> 4)) * 2 + (cc & 1);  // V[e][tile&15][ci>>1][pp][ci&1]
+  // V[e][tile&15][(ci>>1) ^ sw][pp][ci&1], sw = ((tile&15) >> 2) & 2: the A-operand ds_read_b128 is
+  // serviced in four 16-lane groups ({0-3,12-15,20-27}, ...) that the unswizzled slot order put on 8
+  // distinct 16-B bank quads (2-way conflicts); with the swizzle every group covers all 16
+  const int v_off = (((tt & 15) * 4 + ((cc >> 1) ^ (((tt & 15) >> 2) & 2))) * 2 + (tt >> 4)) * 2 + (cc & 1);
   auto transform_read = [&](int rstage, float (&d)[16]) __attribute__((always_inline)) {
     const float* rb = reinterpret_cast<const float*>(raw + rstage * Q_RAW) + raw_off;
 #pragma unroll
@@ -164,7 +173,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int nt = 0; nt < 3; ++nt) acc[j][m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int a_off = (l16 * 4 + q) * 16;
+  const int a_off = (l16 * 4 + (q ^ ((l16 >> 2) & 2))) * 16;
   auto read_a = [&](int vstage, f32x4 (&a)[4]) __attribute__((always_inline)) {
     const char* vb = vbuf + vstage * Q_V + a_off;
 #pragma unroll
