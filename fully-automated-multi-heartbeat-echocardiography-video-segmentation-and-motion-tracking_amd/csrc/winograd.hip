@@ -110,10 +110,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       t[2 * 4 + c] = d[2 * 4 + c] - d[1 * 4 + c];
       t[3 * 4 + c] = d[1 * 4 + c] - d[3 * 4 + c];
     }
-    // V[e][tile & 15][ci >> 1][tile >> 4][ci & 1]: one lane's A operands of both m tiles and both
-    // K steps are 16 contiguous bytes (a conflict-free ds_read_b128)
-    float* vb = reinterpret_cast<float*>(vbuf + buf_v * V_BYTES) + (((tt & 15) * 4 + (cc >> 1)) * 2 + (tt >> 4)) * 2 +
-                (cc & 1);
+    // V[e][tile & 15][(ci >> 1) ^ sw][tile >> 4][ci & 1], sw = ((tile & 15) >> 2) & 2: one lane's A
+    // operands of both m tiles and both K steps are 16 contiguous bytes, and the swizzle puts every
+    // 16-lane group of the ds_read_b128 on distinct bank quads (see conv_wino_q)
+    float* vb = reinterpret_cast<float*>(vbuf + buf_v * V_BYTES) +
+                (((tt & 15) * 4 + ((cc >> 1) ^ (((tt & 15) >> 2) & 2))) * 2 + (tt >> 4)) * 2 + (cc & 1);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {  // (B^T d) B
       vb[(4 * r + 0) * BT * 8] = t[4 * r + 0] - t[4 * r + 2];
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     transform_write(d, 0);
   }
 
-  const int a_off = (l16 * 4 + q) * 16;  // byte offset of the lane's 4 V values inside one e slice
+  const int a_off = (l16 * 4 + (q ^ ((l16 >> 2) & 2))) * 16;  // the lane's 4 V values inside one e slice
   // One chunk k: U(k) is in `uc`, U(k+2) is fetched into `un` (3-way rotation, no register copies);
   // raw(k+3) is fetched into the ring slot raw(k) used; raw(k+1) is transformed into V[(k+1)&1]
   // while the MFMAs consume V[k&1].
