@@ -5,6 +5,21 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// n / d for a runtime divisor d >= 1 and n < 2^31 as one multiply-high and an add (Granlund-Montgomery
+// with a 33-bit multiplier): a per-lane integer division by a kernel argument is a ~30-instruction
+// VALU sequence, and the block prologues / epilogues of the conv kernels decode tile indices with
+// several of them. Exhaustively checked for d < 5000 and sampled up to 2^31 (tools/).
+struct FastDiv {
+  unsigned m;
+  int l;
+};
+inline FastDiv fast_div(unsigned d) {
+  int l = 0;
+  while ((1u << l) < d) ++l;
+  return FastDiv{(unsigned)(((1ull << 32) * ((1ull << l) - d)) / d + 1), l};
+}
+__device__ inline int fdiv(int n, FastDiv f) { return (int)((__umulhi((unsigned)n, f.m) + (unsigned)n) >> f.l); }
+
 // One bias-free conv3d (BN folded into weights/bias) as an implicit GEMM over channels-last
 // activations: Y[m][n] = sum_k A[m][k] * W[n][k] (+bias[n], +res[m][n], relu).
 //   m = ((n*To + to)*Ho + ho)*Wo + wo            (output voxel)

@@ -83,8 +83,13 @@ __device__ inline void epilogue(const ConvParams& p, const f32x4 (&acc)[MT][NT],
 // ---------------------------------------------------------------------------------------------
 // LDS-DMA implicit GEMM. T = float (K step 16) or __bf16 (K step 32). 4 waves along M (BM = 64*MT),
 // BN = 16*NT, S-stage ring. Requires Cin (and Cin2) % (K step) == 0.
+// Fast divisors of the output-voxel decode (m -> wo, ho, to, clip) and of the tile index.
+struct DmaDivs {
+  FastDiv wo, ho, to, nt;
+};
+
 template <typename T, int MT, int NT, int S>
-__global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles) {
+__global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDivs dv) {
   constexpr int EPS = 16 / sizeof(T);  // elements per 16-B slot
   constexpr int BKE = 4 * EPS;         // K elements per step (one 64-B row)
   constexpr int BM = 64 * MT, BN = 16 * NT;
@@ -100,7 +105,8 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int m0 = (tile / n_tiles) * BM, n0 = (tile % n_tiles) * BN;
+  const int tq = fdiv(tile, dv.nt);
+  const int m0 = tq * BM, n0 = (tile - tq * n_tiles) * BN;
   const int q = lane >> 4, l16 = lane & 15;
   constexpr int G[4] = {0, 2, 3, 1};
 
@@ -119,16 +125,14 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles) {
       int m = m0 + idx * 16 + drow;
       const bool ok = m < p.M;
       if (!ok) m = 0;
-      const int wo = m % p.Wo;
-      m /= p.Wo;
-      const int ho = m % p.Ho;
-      m /= p.Ho;
-      const int to = m % p.To;
+      const int mw = fdiv(m, dv.wo), wo = m - mw * p.Wo;
+      const int mh = fdiv(mw, dv.ho), ho = mw - mh * p.Ho;
+      const int mt = fdiv(mh, dv.to), to = mh - mt * p.To;
       d_t[j] = ok ? to * p.st - p.pt : -(1 << 20);  // a row past M never passes the bounds test
       d_h[j] = ho * p.sh - p.ph;
       d_w[j] = wo * p.sw - p.pw;
       // linear input-voxel index of tap (0,0,0); may point outside when padded (never used then)
-      d_pix[j] = (((m / p.To) * p.Ti + d_t[j]) * p.Hi + d_h[j]) * p.Wi + d_w[j];
+      d_pix[j] = ((mt * p.Ti + d_t[j]) * p.Hi + d_h[j]) * p.Wi + d_w[j];
     } else if (idx < T_INS) {
       d_kind[j] = 1;
       d_wrow[j] = w + (size_t)(n0 + (idx - A_INS) * 16 + drow) * p.Kp + EPS * dq;
@@ -278,18 +282,19 @@ __global__ __launch_bounds__(256) void conv_stem_f32(ConvParams p, int n_tiles) 
     a_w[i] = wo * p.sw - p.pw;
   }
   f32x4 ra[AL], rb[BL];
-  const int khw = p.KH * p.KW;
+  // the stem's geometry is fixed (launch_stem checks it): 1x7x7 taps over 4 (3 + pad) channels, so
+  // a float4 K group is exactly one tap and the tap decode is a division by the constant 7
+  constexpr int KW = 7, CIN = 4;
   auto load_tiles = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < AL; ++i) {
       const int k = k0 + 4 * a_q[i];
-      const int tap = k / p.Cin, c = k - tap * p.Cin;
-      const int kt = tap / khw, rem = tap - kt * khw, kh = rem / p.KW, kw = rem - kh * p.KW;
-      const int ti = a_t[i] + kt, hi = a_h[i] + kh, wi = a_w[i] + kw;
-      const bool ok = a_ok[i] && (k < p.K) && (unsigned)ti < (unsigned)p.Ti && (unsigned)hi < (unsigned)p.Hi &&
+      const int tap = k / CIN, kh = tap / KW, kw = tap - kh * KW;
+      const int hi = a_h[i] + kh, wi = a_w[i] + kw;
+      const bool ok = a_ok[i] && (k < p.K) && (unsigned)a_t[i] < (unsigned)p.Ti && (unsigned)hi < (unsigned)p.Hi &&
                       (unsigned)wi < (unsigned)p.Wi;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (ok) v = *reinterpret_cast<const f32x4*>(x + ((((size_t)a_n[i] * p.Ti + ti) * p.Hi + hi) * p.Wi + wi) * p.Cin + c);
+      if (ok) v = *reinterpret_cast<const f32x4*>(x + ((((size_t)a_n[i] * p.Ti + a_t[i]) * p.Hi + hi) * p.Wi + wi) * CIN);
       ra[i] = v;
     }
 #pragma unroll
@@ -458,12 +463,14 @@ template <typename T, int MT, int NT, int S>
 hipError_t launch_dma(const ConvParams& p, hipStream_t s) {
   constexpr int BM = 64 * MT, BN = 16 * NT;
   const int mt = (p.M + BM - 1) / BM, nt = (p.Cout + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_dma<T, MT, NT, S>), dim3(mt * nt), dim3(256), 0, s, p, nt);
+  const DmaDivs dv{fast_div(p.Wo), fast_div(p.Ho), fast_div(p.To), fast_div(nt)};
+  hipLaunchKernelGGL((conv_dma<T, MT, NT, S>), dim3(mt * nt), dim3(256), 0, s, p, nt, dv);
   return hipGetLastError();
 }
 
 template <int NT>
 hipError_t launch_stem(const ConvParams& p, hipStream_t s) {
+  if (p.Cin != 4 || p.KT != 1 || p.KH != 7 || p.KW != 7) return hipErrorInvalidValue;  // conv_stem_f32's geometry
   const int mt = (p.M + 127) / 128, nt = (p.Cout + 16 * NT - 1) / (16 * NT);
   hipLaunchKernelGGL((conv_stem_f32<NT>), dim3(mt * nt), dim3(256), 0, s, p, nt);
   return hipGetLastError();

@@ -66,7 +66,8 @@ static_assert(QPatch<2>::DPW == 3 && QPatch<2>::LDS <= 80 * 1024, "PT = 2 layout
 // output element carried two selects).
 template <int NCH, int PT = 4, int EPI = 2, bool C8 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino_q(ConvParams p, int n_co,
-                                                                                             int n_patches) {
+                                                                                             int n_patches, FastDiv fd_co,
+                                                                                             FastDiv fd_frame, FastDiv fd_px) {
   using G = QPatch<PT>;
   constexpr int Q_RAW = G::RAW, DPW = G::DPW;
   __shared__ __align__(16) char smem[G::LDS];
@@ -80,7 +81,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, l16 = lane & 15;
   const int blk = xcd_swizzle_p(blockIdx.x, gridDim.x);
-  const int pg0 = (blk / n_co) * G::PPB, n0 = (blk % n_co) * 48;
+  const int bq = fdiv(blk, fd_co);
+  const int pg0 = bq * G::PPB, n0 = (blk - bq * n_co) * 48;
   const int H = p.Ho, W = p.Wo, C = p.Cin, CO = p.Cout;
   const int PY = H / (2 * PT), PX = W / (2 * PT);
   const int nchunk = NCH > 0 ? NCH : C >> 3;
@@ -96,8 +98,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const int py = pix / G::SIDE, px = pix - py * G::SIDE;
       const int gp = pg0 + pp;
       if (gp < n_patches && pix < G::PIX) {
-        const int f = gp / (PY * PX), r = gp - f * (PY * PX);
-        const int pr = r / PX, pc = r - pr * PX;
+        const int f = fdiv(gp, fd_frame), r = gp - f * (PY * PX);
+        const int pr = fdiv(r, fd_px), pc = r - pr * PX;
         const int yy = pr * 2 * PT - 1 + py, xx = pc * 2 * PT - 1 + px;
         if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) off = ((f * H + yy) * W + xx) * C + half * 4;
       }
@@ -304,8 +306,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int gp = pg0 + tl / (PT * PT);
     const bool live = un < UNITS && gp < n_patches;
     const int gpc = live ? gp : pg0;
-    const int f = gpc / (PY * PX), r = gpc - f * (PY * PX);
-    const int pr = r / PX, pc = r - pr * PX;
+    const int f = fdiv(gpc, fd_frame), r = gpc - f * (PY * PX);
+    const int pr = fdiv(r, fd_px), pc = r - pr * PX;
     const int yy = pr * 2 * PT + 2 * ((tl / PT) % PT), xx = pc * 2 * PT + 2 * (tl % PT);
     const int co = n0 + 4 * cq;
     const size_t pix = (size_t)(f * H + yy) * W + xx;
@@ -365,15 +367,19 @@ hipError_t launch_qe(const ConvParams& p, hipStream_t s) {
   const int n_patches = p.N * p.To * (p.Ho / (2 * PT)) * (p.Wo / (2 * PT));
   const int n_co = p.Cout / 48;
   const dim3 grid(((n_patches + PPB - 1) / PPB) * n_co);
+  const int px = p.Wo / (2 * PT), py = p.Ho / (2 * PT);
+  const FastDiv fd_co = fast_div(n_co), fd_frame = fast_div(px * py), fd_px = fast_div(px);
   if constexpr (PT == 4) {  // 8-channel-blocked output: 8x8-pixel patches only (engine.hip, c8_pair)
     if (p.y_c8) {
-      hipLaunchKernelGGL((conv_wino_q<NCH, PT, EPI, true>), grid, dim3(256), 0, s, p, n_co, n_patches);
+      hipLaunchKernelGGL((conv_wino_q<NCH, PT, EPI, true>), grid, dim3(256), 0, s, p, n_co, n_patches, fd_co, fd_frame,
+                         fd_px);
       return hipGetLastError();
     }
   } else {
     if (p.y_c8) return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL((conv_wino_q<NCH, PT, EPI, false>), grid, dim3(256), 0, s, p, n_co, n_patches);
+  hipLaunchKernelGGL((conv_wino_q<NCH, PT, EPI, false>), grid, dim3(256), 0, s, p, n_co, n_patches, fd_co, fd_frame,
+                     fd_px);
   return hipGetLastError();
 }
 

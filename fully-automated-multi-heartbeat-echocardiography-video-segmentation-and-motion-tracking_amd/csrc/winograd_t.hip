@@ -276,7 +276,8 @@ struct T5 {
 // EPI: epilogue form, bit 0 = residual add, bit 1 = ReLU (compile-time, no per-element selects).
 template <int TS, int NT, int EPI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_winot5(ConvParams p, int n_co,
-                                                                                             int n_seg, int n_cols) {
+                                                                                             int n_seg, int n_cols,
+                                                                                             FastDiv fd_hw) {
   using G = T5<TS, NT>;
   extern __shared__ __align__(16) char smem[];
   const float* x = reinterpret_cast<const float*>(p.x);
@@ -312,7 +313,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       int gc = col0 + c, t = t_seg - 1 + lf;
       gc = gc < n_cols ? gc : n_cols - 1;
       t = t < 0 ? 0 : (t >= T ? T - 1 : t);
-      const int n = gc / HW, pix = gc - n * HW;
+      const int n = fdiv(gc, fd_hw), pix = gc - n * HW;
       off = (unsigned)(((n * T + t) * HW + pix) * cs + half * 4) * 4u;
     } else if (I < G::NI) {
       const int s = (I - G::RAW_I) * 64 + lane;  // (e, co, stored half)
@@ -403,7 +404,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int gc = col0 + c_rd;
   const bool ok = gc < n_cols;
   const int gcc = ok ? gc : 0;
-  const int n = gcc / HW, pix = gcc - n * HW;
+  const int n = fdiv(gcc, fd_hw), pix = gcc - n * HW;
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     const int t0 = t0w + 4 * m;
@@ -454,7 +455,8 @@ hipError_t winot5_launch_e(const ConvParams& p, hipStream_t s) {
   const int n_seg = (p.Ti / 4) / TS;
   const int n_co = p.Cout / G::CB;
   const int nb = ((n_cols + G::P - 1) / G::P) * n_seg * n_co;
-  hipLaunchKernelGGL((conv_winot5<TS, NT, EPI>), dim3(nb), dim3(256), G::LDS, s, p, n_co, n_seg, n_cols);
+  hipLaunchKernelGGL((conv_winot5<TS, NT, EPI>), dim3(nb), dim3(256), G::LDS, s, p, n_co, n_seg, n_cols,
+                     fast_div(p.Hi * p.Wi));
   return hipGetLastError();
 }
 

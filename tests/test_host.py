@@ -249,3 +249,22 @@ def test_owner_mapping_is_block_aligned():
     assert rows_exchanged(owner_of_clips(plans, 2), 2) == 15
     plans = _plans([10, 40, 10])  # blocks [0,30), [30,60): video 1 has 20 clips in rank 0, 20 in 1 -> 0
     assert video_owners(plans, 2) == [0, 0, 1]
+
+
+def test_fast_division_magic_numbers(tmp_path):
+    """FastDiv (csrc/common.h), the multiply-high division the conv kernels decode tile indices with,
+    equals integer division for every divisor < 5000 and the engine's map sizes (tools/fastdiv_check.cpp
+    restates the same construction on the host)."""
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    src = os.path.join(REPO, "tools", "fastdiv_check.cpp")
+    exe = str(tmp_path / "fdc")
+    subprocess.run([gxx, "-O2", "-std=c++17", src, "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0 and "mismatches: 0" in r.stdout, r.stdout + r.stderr
+    hdr = open(os.path.join(REPO, "fully-automated-multi-heartbeat-echocardiography-video-segmentation-and-motion-tracking_amd",
+                            "csrc", "common.h")).read()
+    assert "(((1ull << 32) * ((1ull << l) - d)) / d + 1)" in hdr  # the construction the check restates
