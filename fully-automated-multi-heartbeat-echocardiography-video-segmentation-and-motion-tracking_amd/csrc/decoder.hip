@@ -32,8 +32,8 @@ constexpr int PIX = 72;
 constexpr int TILE_H = 8, TILE_W = 16;
 // Source window bounds of one 8x16-voxel tile per tap (tap i: scale (in-1)/(out-1) < 2^-(i+1), so
 // 8 rows touch at most floor(7 s) + 3 source rows, 16 columns floor(15 s) + 3).
-__constant__ const int kMaxRows[4] = {6, 4, 3, 3};
-__constant__ const int kMaxCols[4] = {10, 6, 4, 3};
+constexpr int kMaxRows[4] = {6, 4, 3, 3};
+constexpr int kMaxCols[4] = {10, 6, 4, 3};  // also the staging row pitch
 // tap 0 (stem + layer1) keeps the clip's frame rate: its temporal scale is exactly 1, one frame;
 // taps 1-3 read two frames and stage their temporal blend.
 constexpr int kFrames[4] = {1, 2, 2, 2};
@@ -47,6 +47,8 @@ constexpr int kLoads[4] = {(kTapPix[0] * 16 + 255) / 256, (kTapPix[1] * 16 + 255
 constexpr int kLoadOff[4] = {0, kLoads[0] * kFrames[0], kLoads[0] * kFrames[0] + kLoads[1] * kFrames[1],
                              kLoads[0] * kFrames[0] + kLoads[1] * kFrames[1] + kLoads[2] * kFrames[2]};
 constexpr int kLoadsTotal = kLoadOff[3] + kLoads[3] * kFrames[3];
+constexpr int kLiveOff[5] = {0, kLoads[0], kLoads[0] + kLoads[1], kLoads[0] + kLoads[1] + kLoads[2],
+                             kLoads[0] + kLoads[1] + kLoads[2] + kLoads[3]};
 
 struct Win {
   int t0, t1, nf, r0, nr, c0, nc;
@@ -60,6 +62,10 @@ __device__ inline void src_index(float s, int dst, int in, int& i0, int& i1, flo
   i1 = i0 + (i0 < in - 1 ? 1 : 0);
   l0 = 1.f - l1;
 }
+
+// tanh(x) = 1 - 2 / (e^(2x) + 1) on v_exp_f32 and v_rcp_f32: a few VALU instructions instead of
+// tanhf's ~30 (the decoder is VALU-issue bound); absolute error ~1e-7, saturates to +-1 exactly
+__device__ inline float fast_tanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * x) + 1.f); }
 
 __device__ inline int xcd_swizzle_d(int b, int nb) {
   const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
@@ -147,7 +153,7 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
         if (co < 2)
           p.seg[((size_t)n * 2 + co) * TH + pix] = v;
         else
-          p.mot[((size_t)n * 4 + (co - 2)) * TH + pix] = tanhf(v);
+          p.mot[((size_t)n * 4 + (co - 2)) * TH + pix] = fast_tanh(v);
       }
     }
   }
@@ -209,20 +215,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
   // All staging loads are issued before the first LDS write (fixed per-tap trip counts, predicated),
   // so one block waits for one HBM/L2 latency instead of one per 16-byte chunk.
   f32x4 buf[kLoadsTotal];
+  bool live[kLiveOff[4]];  // per (tap, k): the staged element exists in the window
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const DecTap& tp = p.tap[i];
     const Win& w = win[i];
-    const int total = w.nr * w.nc * 16;
+    // staged with the constant row pitch kMaxCols[i] (the decode is a division by a constant;
+    // columns past the window's nc are not loaded and never read)
 #pragma unroll
     for (int k = 0; k < kLoads[i]; ++k) {
       const int e = tid + 256 * k;
+      const int c4 = e & 15, px = e >> 4;
+      const int rr = px / kMaxCols[i], cc = px - rr * kMaxCols[i];
+      const bool lv = e < kTapPix[i] * 16 && rr < w.nr && cc < w.nc;
+      live[kLiveOff[i] + k] = lv;
 #pragma unroll
       for (int f = 0; f < kFrames[i]; ++f) {
         f32x4& v = buf[kLoadOff[i] + k * kFrames[i] + f];
-        if (e < total) {
-          const int c4 = e & 15, px = e >> 4;
-          const int cc = px % w.nc, rr = px / w.nc;
+        if (lv) {
           const int tf = f ? w.t1 : w.t0;
           // 32-bit element offsets (the launcher checks every tap tensor stays below 2^31 floats)
           const int off = (((n * tp.T + tf) * tp.H + (w.r0 + rr)) * tp.W + (w.c0 + cc)) * 64 + c4 * 4;
@@ -234,12 +244,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const Win& w = win[i];
-    const int total = w.nr * w.nc * 16;
     float* dst = stage + kPixOff[i] * PIX;
 #pragma unroll
     for (int k = 0; k < kLoads[i]; ++k) {
       const int e = tid + 256 * k;
-      if (e < total) {
+      if (live[kLiveOff[i] + k]) {
         f32x4 v = buf[kLoadOff[i] + k * kFrames[i]];
         if (kFrames[i] == 2) v = v * w.lt0 + buf[kLoadOff[i] + k * kFrames[i] + 1] * w.lt1;
         *reinterpret_cast<f32x4*>(dst + (e >> 4) * PIX + (e & 15) * 4) = v;
@@ -274,7 +283,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     src_index(tp.sh, hr, tp.H, ya0, ya1, la0, la1);
     src_index(tp.sh, hr + 1, tp.H, yb0, yb1, lb0, lb1);
     const int nrows = yb1 - ya0 + 1;  // 1..3, wave-uniform
-    const float* fb = stage + kPixOff[i] * PIX + 4 * q + (ya0 - w.r0) * w.nc * PIX;
+    const float* fb = stage + kPixOff[i] * PIX + 4 * q + (ya0 - w.r0) * kMaxCols[i] * PIX;
     const float* c0p = fb + (x0 - w.c0) * PIX;
     const float* c1p = fb + (x1 - w.c0) * PIX;
 #pragma unroll
@@ -283,7 +292,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
       // weights of source row ya0 + k in output rows hr (wa) and hr + 1 (wb)
       const float wa = (k == 0 ? la0 : 0.f) + (ya1 - ya0 == k ? la1 : 0.f);
       const float wb = (yb0 - ya0 == k ? lb0 : 0.f) + (yb1 - ya0 == k ? lb1 : 0.f);
-      const int ro = k * w.nc * PIX;
+      const int ro = k * kMaxCols[i] * PIX;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const f32x4 hx = *reinterpret_cast<const f32x4*>(c0p + ro + 16 * c) * lx0 +
@@ -360,7 +369,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         if (co < 2)
           p.seg[((size_t)n * 2 + co) * TH + pix] = v;
         else
-          p.mot[((size_t)n * 4 + (co - 2)) * TH + pix] = tanhf(v);
+          p.mot[((size_t)n * 4 + (co - 2)) * TH + pix] = fast_tanh(v);
       }
     }
   }
