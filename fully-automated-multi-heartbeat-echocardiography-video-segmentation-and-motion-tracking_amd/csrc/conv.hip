@@ -94,7 +94,12 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
   constexpr int BKE = 4 * EPS;         // K elements per step (one 64-B row)
   constexpr int BM = 64 * MT, BN = 16 * NT;
   constexpr int A_INS = BM / 16, B_INS = BN / 16, T_INS = A_INS + B_INS;
-  constexpr int PER_WAVE = (T_INS + 3) / 4;
+  // DMA slot j of wave w: j < A_PER -> A instruction w*A_PER + j; else B instruction w + 4*(j - A_PER)
+  // (past B_INS: the sink). Every slot's kind is a compile-time constant, so the per-step issue code
+  // has no branches on it (a wave-index-dependent kind made the compiler emit both paths per slot).
+  constexpr int A_PER = A_INS / 4, B_PER = (B_INS + 3) / 4;
+  constexpr int PER_WAVE = A_PER + B_PER;
+  static_assert(A_INS % 4 == 0, "A rows split evenly over the 4 waves");
   constexpr int STAGE = T_INS * 1024;  // bytes per ring stage (16 rows x 64 B per DMA instruction)
   constexpr int JUNK = S * STAGE;      // 1 KB sink for the padding DMAs
   __shared__ __align__(16) char smem[S * STAGE + 1024];
@@ -114,14 +119,13 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
   const int drow = lane >> 2;
   const int dq = (lane & 3) ^ G[(drow >> 2) & 3];  // logical slot this lane fetches
   const T* d_wrow[PER_WAVE];
-  int d_t[PER_WAVE], d_h[PER_WAVE], d_w[PER_WAVE], d_pix[PER_WAVE], d_kind[PER_WAVE];  // kind 0 A, 1 B, 2 junk
+  int d_t[PER_WAVE], d_h[PER_WAVE], d_w[PER_WAVE], d_pix[PER_WAVE];  // A rows: tap-(0,0,0) input voxel
 #pragma unroll
   for (int j = 0; j < PER_WAVE; ++j) {
-    const int idx = wid + 4 * j;
+    const int idx = j < A_PER ? wid * A_PER + j : A_INS + wid + 4 * (j - A_PER);
     d_t[j] = d_h[j] = d_w[j] = d_pix[j] = 0;
     d_wrow[j] = w;
-    if (idx < A_INS) {
-      d_kind[j] = 0;
+    if (j < A_PER) {
       int m = m0 + idx * 16 + drow;
       const bool ok = m < p.M;
       if (!ok) m = 0;
@@ -134,10 +138,7 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
       // linear input-voxel index of tap (0,0,0); may point outside when padded (never used then)
       d_pix[j] = ((mt * p.Ti + d_t[j]) * p.Hi + d_h[j]) * p.Wi + d_w[j];
     } else if (idx < T_INS) {
-      d_kind[j] = 1;
       d_wrow[j] = w + (size_t)(n0 + (idx - A_INS) * 16 + drow) * p.Kp + EPS * dq;
-    } else {
-      d_kind[j] = 2;
     }
   }
   const int khw = p.KH * p.KW;
@@ -169,16 +170,18 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
     const T* xc = xb + c0 + EPS * dq;
 #pragma unroll
     for (int j = 0; j < PER_WAVE; ++j) {
-      const int idx = wid + 4 * j;
+      const int idx = j < A_PER ? wid * A_PER + j : A_INS + wid + 4 * (j - A_PER);
       const void* src;
-      if (d_kind[j] == 0) {
+      if (j < A_PER) {
         const int ti = d_t[j] + kt, hi = d_h[j] + kh, wi = d_w[j] + kw;
-        const bool ok = (unsigned)ti < (unsigned)p.Ti && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi;
-        src = ok ? (const void*)(xc + (size_t)(unsigned)(d_pix[j] + tap_pix) * cin) : p.zero;
-      } else if (d_kind[j] == 1) {
-        src = d_wrow[j] + k0;
+        // bitwise &: short-circuit && became nested exec-masked branches
+        const bool ok = ((unsigned)ti < (unsigned)p.Ti) & ((unsigned)hi < (unsigned)p.Hi) & ((unsigned)wi < (unsigned)p.Wi);
+        // element offset in 32 bits (a tensor has < 2^32 elements): one v_mul_lo_u32, where the
+        // 64-bit product was two v_mad_u64_u32
+        const unsigned e = (unsigned)(d_pix[j] + tap_pix) * (unsigned)cin;
+        src = ok ? (const void*)(xc + (size_t)e) : p.zero;
       } else {
-        src = p.zero;
+        src = idx < T_INS ? (const void*)(d_wrow[j] + k0) : p.zero;
       }
       char* dst = (idx < T_INS) ? smem + slot * STAGE + idx * 1024 : smem + JUNK;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
