@@ -78,6 +78,10 @@ void wino_transform_weights(const double* w, int cout, int cin, int cout_p, int 
 // Patch-tiled Winograd F(2x2,3x3) for Ho, Wo % 4 == 0 (winograd2.hip); p.w = conv_wino's U.
 bool winoq_supported(const ConvParams& p);
 hipError_t launch_winoq(const ConvParams& p, hipStream_t s);
+// Barrier-free patch-tiled Winograd F(2x2,3x3) (winograd_w.hip): the conv_wino_q op on 8x8-pixel
+// patches for Cin 64 / 128, bit-identical to it; p.w = conv_wino's U.
+bool winow_supported(const ConvParams& p);
+hipError_t launch_winow(const ConvParams& p, hipStream_t s);
 // Patch-tiled Winograd F(2x4,3x3) (winograd3.hip), Ho, Wo % 8 == 0; p.w = U below.
 bool winor_supported(const ConvParams& p);
 hipError_t launch_winor(const ConvParams& p, hipStream_t s);

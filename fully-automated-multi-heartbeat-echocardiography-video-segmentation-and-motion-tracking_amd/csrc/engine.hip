@@ -300,7 +300,7 @@ double conv_gflop(const Conv& c, const Shape5& out) {
 double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
   const double nt = (double)out.n * out.t;
   const double cc = (double)c.cin_p * c.cout_p;
-  if (!strcmp(kname, "conv_wino_q") || !strcmp(kname, "conv_wino"))
+  if (!strcmp(kname, "conv_wino_q") || !strcmp(kname, "conv_wino_w") || !strcmp(kname, "conv_wino"))
     return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 1) / 2) * 16.0 * cc * 1e-9;
   if (!strcmp(kname, "conv_wino_r")) return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 3) / 4) * 24.0 * cc * 1e-9;
   if (!strcmp(kname, "conv_winot")) return 2.0 * out.n * (out.t / 4) * (double)out.h * out.w * 6.0 * cc * 1e-9;
@@ -345,6 +345,10 @@ const char* pick_kernel(const Conv& c, ConvParams p) {
   if (c.dwinor && getenv("CLASFV_WINO_R") && winor_supported(p)) return "conv_wino_r";
   if (c.dwino) {
     const bool no_patch = getenv("CLASFV_NO_WINO_PATCH") != nullptr;  // A/B switch (tests)
+    // conv_wino_w (barrier-free, bit-identical) is opt-in: measured 2.89 vs 2.31 ms per layer1 launch
+    // (4x the LDS-DMA instructions, paired 32-bank LDS reads, and the compiler drains every LDS-DMA in
+    // flight before the first chunks' reads)
+    if (!no_patch && getenv("CLASFV_WINO_W") && winow_supported(p)) return "conv_wino_w";
     if (!no_patch && winoq_supported(p)) return "conv_wino_q";
     if (wino_supported(p)) return "conv_wino";
   }
@@ -371,7 +375,8 @@ bool c8_pair(const Conv& a, const Conv& b, const Shape5& in) {
   // (layer1) write the blocked layout at no cost while the temporal kernels after them gain 17-24 %;
   // conv_wino_q on 4x4-pixel patches (layer2, 28x28 maps) lost 12 % to its scattered 32-B pieces
   // for a 7 % gain downstream, conv_wino (layer3) broke even: those stay channels-last.
-  const bool writes = (!strcmp(ka, "conv_wino_q") && pa.Ho % 8 == 0 && pa.Wo % 8 == 0) || !strcmp(ka, "conv_stem_f32");
+  const bool writes = ((!strcmp(ka, "conv_wino_q") || !strcmp(ka, "conv_wino_w")) && pa.Ho % 8 == 0 && pa.Wo % 8 == 0) ||
+                      !strcmp(ka, "conv_stem_f32");
   return writes && !a.out_bf16 && !strcmp(pick_kernel(b, pb), "conv_winot") && winot_c8_ok(pb);
 }
 
@@ -389,12 +394,15 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   p.y_c8 = y_c8;
   const char* k = pick_kernel(c, p);
   *kname = k;
-  const bool c8_out = !strcmp(k, "conv_wino_q") || !strcmp(k, "conv_stem_f32");
+  const bool c8_out = !strcmp(k, "conv_wino_q") || !strcmp(k, "conv_wino_w") || !strcmp(k, "conv_stem_f32");
   if ((y_c8 && !c8_out) || (x_c8 && strcmp(k, "conv_winot")))
     return fail(CLASFV_EINVAL, "internal: 8-channel-blocked layout on an unsupported kernel");
   if (!strcmp(k, "conv_wino_r")) {
     p.w = c.dwinor;
     HIP_TRY(launch_winor(p, s));
+  } else if (!strcmp(k, "conv_wino_w")) {
+    p.w = c.dwino;
+    HIP_TRY(launch_winow(p, s));
   } else if (!strcmp(k, "conv_wino_q")) {
     p.w = c.dwino;
     HIP_TRY(launch_winoq(p, s));

@@ -563,6 +563,20 @@ def test_kernel_variants_bitexact(model, monkeypatch, shape):
     assert torch.equal(s_new, s_old) and torch.equal(m_new, m_old)
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (1, 3, 8, 224, 224)])
+def test_wino_w_matches_wino_q_bitexact(model, monkeypatch, shape):
+    """The barrier-free conv_wino_w (opt-in with CLASFV_WINO_W=1; layer1 at 112x112 clips, layer1 +
+    layer2 at 224x224) computes conv_wino_q's products in conv_wino_q's order: the forward is
+    bit-identical with it switched on."""
+    rng = np.random.default_rng(37)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    s_q, m_q = model(x)
+    monkeypatch.setenv("CLASFV_WINO_W", "1")
+    s_w, m_w = model(x)
+    monkeypatch.delenv("CLASFV_WINO_W")
+    assert torch.equal(s_w, s_q) and torch.equal(m_w, m_q)
+
+
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (1, 3, 8, 32, 48)])
 def test_c8_blocked_mid_bitexact(model, monkeypatch, shape):
     """The 8-channel-blocked mid tensors (stem and Conv2Plus1D spatial -> temporal Winograd) only

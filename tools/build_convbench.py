@@ -10,7 +10,7 @@ REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 import clasfv_amd.build as B  # noqa: E402
 
-KERNELS = ["winograd.hip", "winograd2.hip", "winograd3.hip", "winograd_t.hip", "conv.hip", "conv_patch.hip",
+KERNELS = ["winograd.hip", "winograd2.hip", "winograd3.hip", "winograd_t.hip", "winograd_w.hip", "conv.hip", "conv_patch.hip",
            "decoder.hip"]
 
 
