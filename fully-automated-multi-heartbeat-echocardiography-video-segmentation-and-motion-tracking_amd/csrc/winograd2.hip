@@ -302,7 +302,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int u = 0; u < UPT; ++u) {
     const int un = tid + 256 * u;
-    const int tl = un / CQ, cq = un - tl * CQ;
+    // channels-last: (tile, 4-channel group) with the groups fastest (192-B runs per pixel); C8:
+    // tiles fastest, so a wave's store covers one 8-channel plane's pixels of all 32 tiles and the
+    // two 16-B halves of every 32-B pixel come from the same instruction
+    const int tl = C8 ? un % Q_BT : un / CQ, cq = C8 ? un / Q_BT : un - tl * CQ;
     const int gp = pg0 + tl / (PT * PT);
     const bool live = un < UNITS && gp < n_patches;
     const int gpc = live ? gp : pg0;
@@ -369,7 +372,7 @@ hipError_t launch_qe(const ConvParams& p, hipStream_t s) {
   const dim3 grid(((n_patches + PPB - 1) / PPB) * n_co);
   const int px = p.Wo / (2 * PT), py = p.Ho / (2 * PT);
   const FastDiv fd_co = fast_div(n_co), fd_frame = fast_div(px * py), fd_px = fast_div(px);
-  if constexpr (PT == 4) {  // 8-channel-blocked output: 8x8-pixel patches only (engine.hip, c8_pair)
+  if constexpr (EPI == 2) {  // 8-channel-blocked output: the Conv2Plus1D spatial half (engine.hip, c8_pair)
     if (p.y_c8) {
       hipLaunchKernelGGL((conv_wino_q<NCH, PT, EPI, true>), grid, dim3(256), 0, s, p, n_co, n_patches, fd_co, fd_frame,
                          fd_px);
