@@ -341,7 +341,7 @@ ConvParams conv_params(const Conv& c, const Shape5& in, Shape5& out) {
 // The kernel run_conv launches for c with parameters p (the A/B switches are read here).
 const char* pick_kernel(const Conv& c, ConvParams p) {
   // F(2x4,3x3) is opt-in: 25 % fewer MFMAs than conv_wino_q but 1.5x its U operand traffic per
-  // output; measured slower on layer1 (2.80 vs 2.40 ms, DESIGN.md section 8)
+  // output; measured slower on layer1 (2.80 vs 2.40 ms, DESIGN.md section 7)
   if (c.dwinor && getenv("CLASFV_WINO_R") && winor_supported(p)) return "conv_wino_r";
   if (c.dwino) {
     const bool no_patch = getenv("CLASFV_NO_WINO_PATCH") != nullptr;  // A/B switch (tests)
