@@ -43,7 +43,8 @@ __device__ inline int xcd_swizzle_w(int b, int nb) {
 // fetches too, one chunk early).
 template <int NT, int NCH = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino(ConvParams p, int n_co,
-                                                                                             int n_tiles) {
+                                                                                             int n_tiles, FastDiv fd_f,
+                                                                                             FastDiv fd_x) {
   __shared__ __align__(16) char smem[RAW_STAGES * RAW_BYTES + 2 * V_BYTES];
   char* raw = smem;
   char* vbuf = smem + RAW_STAGES * RAW_BYTES;
@@ -75,8 +76,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int tg = t0 + tl;
     int off = -1;
     if (tg < n_tiles) {
-      const int f = tg / (TY * TX), r = tg - f * (TY * TX);
-      const int ty = r / TX, tx = r - ty * TX;
+      const int f = fdiv(tg, fd_f), r = tg - f * (TY * TX);
+      const int ty = fdiv(r, fd_x), tx = r - ty * TX;
       const int yy = 2 * ty - 1 + (px >> 2), xx = 2 * tx - 1 + (px & 3);
       if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) off = ((f * H + yy) * W + xx) * C + half * 4;
     }
@@ -251,8 +252,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int tg = t0 + tl;
     const bool live = un < UNITS && tg < n_tiles;
     const int tgc = live ? tg : t0;
-    const int f = tgc / (TY * TX), rem = tgc - f * (TY * TX);
-    const int ty = rem / TX, tx = rem - ty * TX;
+    const int f = fdiv(tgc, fd_f), rem = tgc - f * (TY * TX);
+    const int ty = fdiv(rem, fd_x), tx = rem - ty * TX;
     const int co = n0 + 4 * cq;
     u_o[u] = ((size_t)(f * H + 2 * ty) * W + 2 * tx) * CO + co;
     u_z[u] = tl * (16 * NT) + 4 * cq;
@@ -329,10 +330,14 @@ hipError_t launch_wino(const ConvParams& p, hipStream_t s) {
   const int n_tiles = p.N * p.To * ((p.Ho + 1) / 2) * ((p.Wo + 1) / 2);
   const int n_co = p.Cout / 48;
   const int nb = (n_tiles + BT - 1) / BT;
-  switch (p.Cin >> 3) {  // fully unrolled chunk loops for the layer1 / layer2 widths
-    case 8: hipLaunchKernelGGL((conv_wino<3, 8>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
-    case 16: hipLaunchKernelGGL((conv_wino<3, 16>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
-    default: hipLaunchKernelGGL((conv_wino<3, 0>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles); break;
+  const int tx = (p.Wo + 1) / 2, ty = (p.Ho + 1) / 2;
+  const FastDiv fd_f = fast_div(tx * ty), fd_x = fast_div(tx);
+  switch (p.Cin >> 3) {  // fully unrolled chunk loops for the layer1..4 widths
+    case 8: hipLaunchKernelGGL((conv_wino<3, 8>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles, fd_f, fd_x); break;
+    case 16: hipLaunchKernelGGL((conv_wino<3, 16>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles, fd_f, fd_x); break;
+    case 32: hipLaunchKernelGGL((conv_wino<3, 32>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles, fd_f, fd_x); break;
+    case 64: hipLaunchKernelGGL((conv_wino<3, 64>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles, fd_f, fd_x); break;
+    default: hipLaunchKernelGGL((conv_wino<3, 0>), dim3(nb * n_co), dim3(256), 0, s, p, n_co, n_tiles, fd_f, fd_x); break;
   }
   return hipGetLastError();
 }
@@ -343,7 +348,9 @@ hipError_t launch_wino_ko(const ConvParams& p, hipStream_t s, int ko) {
   if (ko != 100) return launch_wino(p, s);
   const int n_tiles = p.N * p.To * ((p.Ho + 1) / 2) * ((p.Wo + 1) / 2);
   const int n_co = p.Cout / 48;
-  hipLaunchKernelGGL((conv_wino<3, 0>), dim3(((n_tiles + BT - 1) / BT) * n_co), dim3(256), 0, s, p, n_co, n_tiles);
+  const int tx = (p.Wo + 1) / 2, ty = (p.Ho + 1) / 2;
+  hipLaunchKernelGGL((conv_wino<3, 0>), dim3(((n_tiles + BT - 1) / BT) * n_co), dim3(256), 0, s, p, n_co, n_tiles,
+                     fast_div(tx * ty), fast_div(tx));
   return hipGetLastError();
 }
 #endif
