@@ -83,12 +83,9 @@ __device__ inline void for_taps(std::integer_sequence<int, I...>, F&& f) {
 
 // S = B ring depth (B(s) is fetched S-1 steps ahead); OCC = blocks per CU (the LDS budget and the
 // register cap follow from it).
-// GT > 1: persistent over GT consecutive output tiles of one n tile -- the next tile's first patch
-// and weight steps stream in under the current tile's last chunk, so only a block's first tile pays
-// the DMA round trip (at Cin = 64 a tile is 18 K steps).
-template <int NT, int KT, int FR, int S, int OCC, int GT>
+template <int NT, int KT, int FR, int S, int OCC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void conv_patch_bf16(
-    ConvParams p, int n_tiles, int ptw, int npt, int t_tiles, int n_lin) {
+    ConvParams p, int n_tiles, int ptw, int npt, int t_tiles) {
   using G = PGeo<KT, FR>;
   constexpr int TAPS = G::TAPS, MT = G::MT;
   static_assert(S >= 2 && S <= TAPS + 1, "wait counts below assume S - 1 <= TAPS");
@@ -102,55 +99,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, l16 = lane & 15;
-  const int bt = xcd_swizzle_p(blockIdx.x, gridDim.x);
-  const int n0 = (bt % n_tiles) * 16 * NT;
-  const int lin0 = (bt / n_tiles) * GT;  // first output tile (clip, t tile, pixel tile) of the block
+  int tile = xcd_swizzle_p(blockIdx.x, gridDim.x);
+  const int n0 = (tile % n_tiles) * 16 * NT;
+  tile /= n_tiles;
+  const int pt = tile % npt;
+  tile /= npt;
+  const int t0 = (tile % t_tiles) * FR;
+  const int clip = tile / t_tiles;
   const int HW = p.Hi * p.Wi;
+  const int h0 = G::SPATIAL ? (pt / ptw) * 8 : 0, w0 = G::SPATIAL ? (pt % ptw) * 8 : 0;
+  const int hw0 = G::SPATIAL ? 0 : pt * 64;
   const int Cin = p.Cin;
-  struct Tile {
-    int t0, clip, h0, w0, hw0;
-  };
-  auto decode = [&](int lin) __attribute__((always_inline)) {
-    Tile tl;
-    const int pt = lin % npt, r = lin / npt;
-    tl.t0 = (r % t_tiles) * FR;
-    tl.clip = r / t_tiles;
-    tl.h0 = G::SPATIAL ? (pt / ptw) * 8 : 0;
-    tl.w0 = G::SPATIAL ? (pt % ptw) * 8 : 0;
-    tl.hw0 = G::SPATIAL ? 0 : pt * 64;
-    return tl;
-  };
 
   // patch DMA: piece j = wid + 4*i writes pixels 16j .. 16j+15, lane -> pixel 16j + lane/4,
   // physical slot lane & 3 (fetches logical slot (lane & 3) ^ g); pieces past the patch land in
   // the sink, pixels outside the map read the zero block
+  int pv[PW];
   unsigned psl[PW];
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
     const int pix = (wid + 4 * i) * 16 + (lane >> 2);
     psl[i] = (unsigned)(((lane & 3) ^ gsw((pix >> 2) & 3)) * 16);
-  }
-  // per-lane source voxel of each patch piece for output tile tl (-1: outside the map -> zeros)
-  auto patch_src = [&](const Tile& tl, int (&pv)[PW]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const int pix = (wid + 4 * i) * 16 + (lane >> 2);
-      pv[i] = -1;
-      if (pix < G::PPIX) {
-        const int f = pix / G::FPIX, r = pix - f * G::FPIX;
-        if constexpr (G::SPATIAL) {
-          const int pr = r / G::PC, pc = r - pr * G::PC;
-          const int ti = tl.t0 + f, hi = tl.h0 - 1 + pr, wi = tl.w0 - 1 + pc;
-          if (ti < p.Ti && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi)
-            pv[i] = ((tl.clip * p.Ti + ti) * p.Hi + hi) * p.Wi + wi;
-        } else {
-          const int ti = tl.t0 - 1 + f, hw = tl.hw0 + r;
-          if ((unsigned)ti < (unsigned)p.Ti && hw < HW) pv[i] = (tl.clip * p.Ti + ti) * HW + hw;
-        }
+    pv[i] = -1;
+    if (pix < G::PPIX) {
+      const int f = pix / G::FPIX, r = pix - f * G::FPIX;
+      if constexpr (G::SPATIAL) {
+        const int pr = r / G::PC, pc = r - pr * G::PC;
+        const int ti = t0 + f, hi = h0 - 1 + pr, wi = w0 - 1 + pc;
+        if (ti < p.Ti && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi)
+          pv[i] = ((clip * p.Ti + ti) * p.Hi + hi) * p.Wi + wi;
+      } else {
+        const int ti = t0 - 1 + f, hw = hw0 + r;
+        if ((unsigned)ti < (unsigned)p.Ti && hw < HW) pv[i] = (clip * p.Ti + ti) * HW + hw;
       }
     }
-  };
-  auto issue_patch = [&](const int (&pv)[PW], int c, int buf) __attribute__((always_inline)) {
+  }
+  auto issue_patch = [&](int c, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
       const int j = wid + 4 * i;
@@ -184,6 +168,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   };
 
   f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // A fragment i of this lane: block voxel m = 16*(MT*wid + i) + l16; LDS byte address of its
   // 16-B slot q at every tap (patch buffer 0)
@@ -200,107 +188,83 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   }
   const int b_rd = B0 + l16 * 64 + (q ^ gsw(l16 >> 2)) * 16;
 
-  const int n_t = min(GT, n_lin - lin0);  // tiles of this block (wave-uniform)
-  Tile cur = decode(lin0);
-  {
-    int pv[PW];  // recomputed per issue (a copy held across the tile loop spilled at NT = 10)
-    patch_src(cur, pv);
-    issue_patch(pv, 0, 0);
-  }
+  issue_patch(0, 0);
 #pragma unroll
   for (int k = 0; k < S - 1; ++k) issue_b(k / TAPS, k % TAPS, k);
   int slot = 0;  // ring slot of B(s) (wave-uniform)
-  int cg = 0;    // chunks done by the block (patch buffer parity)
 
-  for (int g = 0; g < n_t; ++g) {
-    const bool next_tile = g + 1 < n_t;
-    const Tile nxt = decode(next_tile ? lin0 + g + 1 : lin0 + g);
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int c = 0; c < nc; ++c, ++cg) {
-      // a next chunk exists (this tile's, or the next tile's chunk 0)
-      const bool more = c + 1 < nc || next_tile;
-      const int pbuf = (cg & 1) * G::BYTES;
-      for_taps(std::make_integer_sequence<int, TAPS>{}, [&](auto tc) __attribute__((always_inline)) {
-        constexpr int TAP = decltype(tc)::value;
-        // B(s) landed; in flight may stay B(s+1) .. B(s+S-2) and, at taps 1 .. S-1, the next chunk's
-        // patch (issued at tap 0 after B(s)). At tap 0 the chunk's own patch was issued TAPS steps
-        // ago, before B(s) whenever S - 1 <= TAPS.
-        if constexpr (TAP >= 1 && TAP <= S - 1) {
-          if (more) vm_wait<(S - 2) * BW + PW>();
-          else vm_wait<(S - 2) * BW>();
-        } else {
-          vm_wait<(S - 2) * BW>();
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        // B(c + C2, T2): chunk nc is the next tile's chunk 0 (same n tile, same weights)
-        constexpr int T2 = (TAP + S - 1) % TAPS, C2 = (TAP + S - 1) / TAPS;
-        const int slot_new = slot == 0 ? S - 1 : slot - 1;  // (s + S - 1) % S
-        issue_b(c + C2 < nc ? c + C2 : c + C2 - nc, T2, slot_new);
-        if constexpr (TAP == 0) {
-          if (more) {
-            int pv[PW];
-            const bool same = c + 1 < nc;
-            patch_src(same ? cur : nxt, pv);
-            issue_patch(pv, same ? c + 1 : 0, (cg + 1) & 1);
-          }
-        }
-        bf16x8 a[MT], b[NT];
-#pragma unroll
-        for (int i = 0; i < MT; ++i) a[i] = *reinterpret_cast<const bf16x8*>(smem + pbuf + aaddr[TAP][i]);
-        const char* bs = smem + b_rd + slot * B_STAGE;
-#pragma unroll
-        for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + j * 1024);
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-          for (int i = 0; i < MT; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-        slot = slot + 1 == S ? 0 : slot + 1;
-      });
-    }
-
-    // epilogue of tile g: acc[i][j] holds channels n0 + 16j + 4q .. +3 of block voxel 16*(MT*wid + i) + l16
-    const __bf16* res = reinterpret_cast<const __bf16*>(p.res);
-    __bf16* y = reinterpret_cast<__bf16*>(p.y);
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const int m = 16 * (MT * wid + i) + l16, f = m >> 6, px = m & 63;
-      const int to = cur.t0 + f;
-      size_t gm;
-      if constexpr (G::SPATIAL) {
-        const int ho = cur.h0 + (px >> 3), wo = cur.w0 + (px & 7);
-        if (!(to < p.To && ho < p.Ho && wo < p.Wo)) continue;
-        gm = (((size_t)cur.clip * p.To + to) * p.Ho + ho) * p.Wo + wo;
+  for (int c = 0; c < nc; ++c) {
+    const bool more = c + 1 < nc;
+    const int pbuf = (c & 1) * G::BYTES;
+    for_taps(std::make_integer_sequence<int, TAPS>{}, [&](auto tc) __attribute__((always_inline)) {
+      constexpr int TAP = decltype(tc)::value;
+      // B(s) landed; in flight may stay B(s+1) .. B(s+S-2) and, at taps 1 .. S-1, the next chunk's
+      // patch (issued at tap 0 after B(s)). At tap 0 the chunk's own patch was issued TAPS steps
+      // ago, before B(s) whenever S - 1 <= TAPS.
+      if constexpr (TAP >= 1 && TAP <= S - 1) {
+        if (more) vm_wait<(S - 2) * BW + PW>();
+        else vm_wait<(S - 2) * BW>();
       } else {
-        const int hw = cur.hw0 + px;
-        if (!(to < p.To && hw < HW)) continue;
-        gm = ((size_t)cur.clip * p.To + to) * HW + hw;
+        vm_wait<(S - 2) * BW>();
       }
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int n = n0 + j * 16 + 4 * q;
-        const size_t o = gm * p.Cout + n;
-        f32x4 v = acc[i][j];
-        if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
-        if (res) {
-          const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + o);
-          v += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
-        }
-        if (p.relu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        }
-        *reinterpret_cast<bf16x4*>(y + o) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int T2 = (TAP + S - 1) % TAPS, C2 = (TAP + S - 1) / TAPS;
+      const int slot_new = slot == 0 ? S - 1 : slot - 1;  // (s + S - 1) % S
+      issue_b(c + C2, T2, slot_new);
+      if constexpr (TAP == 0) {
+        if (more) issue_patch(c + 1, (c + 1) & 1);
       }
-    }
-    cur = nxt;
+      bf16x8 a[MT], b[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a[i] = *reinterpret_cast<const bf16x8*>(smem + pbuf + aaddr[TAP][i]);
+      const char* bs = smem + b_rd + slot * B_STAGE;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + j * 1024);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      slot = slot + 1 == S ? 0 : slot + 1;
+    });
   }
   vm_wait<0>();  // the past-the-end B fetches land before the block's LDS is released
+
+  // epilogue: acc[i][j] holds channels n0 + 16j + 4q .. +3 of block voxel 16*(MT*wid + i) + l16
+  const __bf16* res = reinterpret_cast<const __bf16*>(p.res);
+  __bf16* y = reinterpret_cast<__bf16*>(p.y);
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = 16 * (MT * wid + i) + l16, f = m >> 6, px = m & 63;
+    const int to = t0 + f;
+    size_t gm;
+    if constexpr (G::SPATIAL) {
+      const int ho = h0 + (px >> 3), wo = w0 + (px & 7);
+      if (!(to < p.To && ho < p.Ho && wo < p.Wo)) continue;
+      gm = (((size_t)clip * p.To + to) * p.Ho + ho) * p.Wo + wo;
+    } else {
+      const int hw = hw0 + px;
+      if (!(to < p.To && hw < HW)) continue;
+      gm = ((size_t)clip * p.To + to) * HW + hw;
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = n0 + j * 16 + 4 * q;
+      const size_t o = gm * p.Cout + n;
+      f32x4 v = acc[i][j];
+      if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
+      if (res) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + o);
+        v += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      *reinterpret_cast<bf16x4*>(y + o) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    }
+  }
 }
 
 template <int NT, int KT, int FR, int S>
@@ -328,26 +292,12 @@ PatchGrid patch_grid(const ConvParams& p, int fr) {
   return g;
 }
 
-// 4 output tiles per block when that still leaves >= 4 rounds of the chip's OCC x 256 block slots;
-// not for the 1x3x3 kernels at NT 9 / 10, whose persistent form spills at their 168-VGPR cap
-// (CLASFV_PATCH_NOPERSIST=1: one tile per block, A/B switch)
 template <int NT, int KT, int FR, int S = 3>
 hipError_t launch_p(const ConvParams& p, hipStream_t s) {
   const PatchGrid g = patch_grid(p, FR);
   const int n_tiles = p.Cout / (16 * NT);
-  constexpr int OCC = patch_occ<NT, KT, FR, S>();
-  constexpr bool PERSIST_OK = KT == 3 || NT <= 8;
-  const long slots = 256L * OCC;
-  const long per_n = g.base;
-  const bool no_persist = getenv("CLASFV_PATCH_NOPERSIST") != nullptr;
-  if (PERSIST_OK && !no_persist && per_n * n_tiles >= 4 * 4 * slots) {
-    const long nb = (per_n + 3) / 4 * n_tiles;
-    hipLaunchKernelGGL((conv_patch_bf16<NT, KT, FR, S, OCC, PERSIST_OK ? 4 : 1>), dim3((unsigned)nb), dim3(256), 0, s, p,
-                       n_tiles, g.ptw, g.npt, g.tt, (int)per_n);
-  } else {
-    hipLaunchKernelGGL((conv_patch_bf16<NT, KT, FR, S, OCC, 1>), dim3((unsigned)(per_n * n_tiles)), dim3(256), 0, s, p,
-                       n_tiles, g.ptw, g.npt, g.tt, (int)per_n);
-  }
+  hipLaunchKernelGGL((conv_patch_bf16<NT, KT, FR, S, patch_occ<NT, KT, FR, S>()>), dim3((unsigned)(g.base * n_tiles)),
+                     dim3(256), 0, s, p, n_tiles, g.ptw, g.npt, g.tt);
   return hipGetLastError();
 }
 

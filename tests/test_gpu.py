@@ -563,23 +563,6 @@ def test_kernel_variants_bitexact(model, monkeypatch, shape):
     assert torch.equal(s_new, s_old) and torch.equal(m_new, m_old)
 
 
-@pytest.mark.parametrize("shape", [(24, 3, 32, 112, 112)])
-def test_patch_bf16_persistent_bitexact(monkeypatch, shape):
-    """bf16 engine: the persistent conv_patch_bf16 (4 output tiles per block on grids of >= 16 rounds:
-    the 3x1x1 convs of 24 or more 112x112 clips)
-    computes every tile's products in the same order as one tile per block
-    (CLASFV_PATCH_NOPERSIST=1): bit-identical forward."""
-    from clasfv_amd.model import R2plus1D_18_MotionNet
-    m16 = R2plus1D_18_MotionNet(pretrained=False, dtype="bf16")
-    rng = np.random.default_rng(41)
-    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
-    s_p, m_p = m16(x)
-    monkeypatch.setenv("CLASFV_PATCH_NOPERSIST", "1")
-    s_1, m_1 = m16(x)
-    monkeypatch.delenv("CLASFV_PATCH_NOPERSIST")
-    assert torch.equal(s_p, s_1) and torch.equal(m_p, m_1)
-
-
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (1, 3, 8, 224, 224)])
 def test_wino_w_matches_wino_q_bitexact(model, monkeypatch, shape):
     """The barrier-free conv_wino_w (opt-in with CLASFV_WINO_W=1; layer1 at 112x112 clips, layer1 +
