@@ -67,6 +67,11 @@ __device__ inline void src_index(float s, int dst, int in, int& i0, int& i1, flo
 // tanhf's ~30 (the decoder is VALU-issue bound); absolute error ~1e-7, saturates to +-1 exactly
 __device__ inline float fast_tanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * x) + 1.f); }
 
+// block- / wave-uniform values computed on the VALU, moved to SGPRs: the address arithmetic and the
+// branches that use them become scalar
+__device__ inline int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ inline float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+
 __device__ inline int xcd_swizzle_d(int b, int nb) {
   const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
@@ -113,7 +118,7 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
     const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 a = bb;  // the bias rides in the accumulator
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl_[kb], hh[mt][kb], a, 0, 0, 0);
@@ -121,7 +126,7 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh_[kb], hh[mt][kb], a, 0, 0, 0);
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) a[r] = fmaxf(a[r] + bb[r], 0.f);
+      for (int r = 0; r < 4; ++r) a[r] = fmaxf(a[r], 0.f);
       acc[mt][nt] = a;  // h2^T[ch = 16nt + 4q + r][voxel l16]
     }
   }
@@ -133,12 +138,15 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
     wh[nt] = *reinterpret_cast<const f32x4*>(p.wh + (l16 & 7) * 64 + 16 * nt + 4 * q);
     if (l16 >= 8) wh[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  f32x4 hb;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) hb[r] = 4 * q + r < 6 ? p.bh[4 * q + r] : 0.f;
   const size_t HW = (size_t)p.H * p.W;
   const size_t TH = (size_t)p.T * HW;
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     const int hr = h0 + 2 * wid + mt;
-    f32x4 out = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 out = hb;  // head bias (rows 4q + r < 6) in the accumulator
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
@@ -149,7 +157,7 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
       for (int r = 0; r < 4; ++r) {
         const int co = 4 * q + r;
         if (co >= 6) continue;
-        const float v = out[r] + p.bh[co];
+        const float v = out[r];
         if (co < 2)
           p.seg[((size_t)n * 2 + co) * TH + pix] = v;
         else
@@ -192,24 +200,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     int a, b;
     float la, lb;
     src_index(tp.st, t, tp.T, a, b, la, lb);
-    w.t0 = a;
-    w.t1 = b;
-    w.lt0 = la;
-    w.lt1 = lb;
-    w.nf = (lb > 0.f && b != a) ? min(2, kFrames[i]) : 1;
-    if (w.nf == 1) {  // single source frame: the blend below is then exactly P[t0]
-      w.t1 = a;
-      w.lt0 = 1.f;
-      w.lt1 = 0.f;
-    }
+    const bool two = lb > 0.f && b != a && kFrames[i] == 2;  // else the blend below is exactly P[t0]
+    w.t0 = uni(a);
+    w.t1 = uni(two ? b : a);
+    w.lt0 = unif(two ? la : 1.f);
+    w.lt1 = unif(two ? lb : 0.f);
+    w.nf = two ? 2 : 1;
     const int r0 = min((int)floorf(tp.sh * (float)h0), tp.H - 1);
     const int r1 = min((int)floorf(tp.sh * (float)(h0 + TILE_H - 1)) + 1, tp.H - 1);
     const int c0 = min((int)floorf(tp.sw * (float)w0), tp.W - 1);
     const int c1 = min((int)floorf(tp.sw * (float)(w0 + TILE_W - 1)) + 1, tp.W - 1);
-    w.r0 = r0;
-    w.nr = min(r1 - r0 + 1, kMaxRows[i]);
-    w.c0 = c0;
-    w.nc = min(c1 - c0 + 1, kMaxCols[i]);
+    w.r0 = uni(r0);
+    w.nr = uni(min(r1 - r0 + 1, kMaxRows[i]));
+    w.c0 = uni(c0);
+    w.nc = uni(min(c1 - c0 + 1, kMaxCols[i]));
     win[i] = w;
   }
   // All staging loads are issued before the first LDS write (fixed per-tap trip counts, predicated),
@@ -222,6 +226,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     const Win& w = win[i];
     // staged with the constant row pitch kMaxCols[i] (the decode is a division by a constant;
     // columns past the window's nc are not loaded and never read)
+    // 32-bit element offsets (the launcher checks every tap tensor stays below 2^31 floats): the
+    // window origin of each source frame is scalar, the per-lane part one multiply per element
+    const int base0 = (((n * tp.T + w.t0) * tp.H + w.r0) * tp.W + w.c0) * 64;
+    const int base1 = base0 + (w.t1 - w.t0) * tp.H * tp.W * 64;
 #pragma unroll
     for (int k = 0; k < kLoads[i]; ++k) {
       const int e = tid + 256 * k;
@@ -229,15 +237,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
       const int rr = px / kMaxCols[i], cc = px - rr * kMaxCols[i];
       const bool lv = e < kTapPix[i] * 16 && rr < w.nr && cc < w.nc;
       live[kLiveOff[i] + k] = lv;
+      const int lo = (rr * tp.W + cc) * 64 + c4 * 4;
 #pragma unroll
       for (int f = 0; f < kFrames[i]; ++f) {
         f32x4& v = buf[kLoadOff[i] + k * kFrames[i] + f];
-        if (lv) {
-          const int tf = f ? w.t1 : w.t0;
-          // 32-bit element offsets (the launcher checks every tap tensor stays below 2^31 floats)
-          const int off = (((n * tp.T + tf) * tp.H + (w.r0 + rr)) * tp.W + (w.c0 + cc)) * 64 + c4 * 4;
-          v = *reinterpret_cast<const f32x4*>(tp.p + off);
-        }
+        if (lv) v = *reinterpret_cast<const f32x4*>(tp.p + (f ? base1 : base0) + lo);
       }
     }
   }
@@ -282,6 +286,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     src_index(tp.sw, w0 + l16, tp.W, x0, x1, lx0, lx1);
     src_index(tp.sh, hr, tp.H, ya0, ya1, la0, la1);
     src_index(tp.sh, hr + 1, tp.H, yb0, yb1, lb0, lb1);
+    ya0 = uni(ya0), ya1 = uni(ya1), yb0 = uni(yb0), yb1 = uni(yb1);
+    la0 = unif(la0), la1 = unif(la1), lb0 = unif(lb0), lb1 = unif(lb1);
     const int nrows = yb1 - ya0 + 1;  // 1..3, wave-uniform
     const float* fb = stage + kPixOff[i] * PIX + 4 * q + (ya0 - w.r0) * kMaxCols[i] * PIX;
     const float* c0p = fb + (x0 - w.c0) * PIX;
@@ -290,15 +296,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     for (int k = 0; k < 3; ++k) {
       if (k >= nrows) break;
       // weights of source row ya0 + k in output rows hr (wa) and hr + 1 (wb)
+      // source row ya0 + k feeds output row hr (ta) / hr + 1 (tb); a row that feeds only one of them
+      // (the outer rows when nrows = 3) skips the other's update, whose weight is exactly 0 (scalar
+      // branches: every condition is wave-uniform)
+      const bool ta = k == 0 || ya1 - ya0 == k, tb = yb0 - ya0 == k || yb1 - ya0 == k;
       const float wa = (k == 0 ? la0 : 0.f) + (ya1 - ya0 == k ? la1 : 0.f);
       const float wb = (yb0 - ya0 == k ? lb0 : 0.f) + (yb1 - ya0 == k ? lb1 : 0.f);
       const int ro = k * kMaxCols[i] * PIX;
+      f32x4 hx[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const f32x4 hx = *reinterpret_cast<const f32x4*>(c0p + ro + 16 * c) * lx0 +
-                         *reinterpret_cast<const f32x4*>(c1p + ro + 16 * c) * lx1;
-        h1[0][c] += hx * wa;
-        h1[1][c] += hx * wb;
+      for (int c = 0; c < 4; ++c)
+        hx[c] = *reinterpret_cast<const f32x4*>(c0p + ro + 16 * c) * lx0 +
+                *reinterpret_cast<const f32x4*>(c1p + ro + 16 * c) * lx1;
+      if (ta) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) h1[0][c] += hx[c] * wa;
+      }
+      if (tb) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) h1[1][c] += hx[c] * wb;
       }
       // one source row's 8 LDS reads in flight at a time (hoisting more spills)
       __builtin_amdgcn_sched_barrier(0);
@@ -330,7 +346,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[mt][nt] = bb;  // the bias rides in the accumulator
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -338,7 +354,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[c][j], h1[mt][c][j], acc[mt][nt], 0, 0, 0);
       // acc[mt][nt][r] = h2^T[ch = 16nt + 4q + r][voxel l16]
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[mt][nt][r] = fmaxf(acc[mt][nt][r] + bb[r], 0.f);
+      for (int r = 0; r < 4; ++r) acc[mt][nt][r] = fmaxf(acc[mt][nt][r], 0.f);
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) wa[c] = wn[c];
@@ -350,10 +366,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
     wh[nt] = *reinterpret_cast<const f32x4*>(p.wh + (l16 & 7) * 64 + 16 * nt + 4 * q);
     if (l16 >= 8) wh[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  f32x4 hb;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) hb[r] = 4 * q + r < 6 ? p.bh[4 * q + r] : 0.f;
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     const int hr = h0 + 2 * wid + mt;
-    f32x4 out = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 out = hb;  // head bias (rows 4q + r < 6) in the accumulator
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
@@ -365,7 +384,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
       for (int r = 0; r < 4; ++r) {
         const int co = 4 * q + r;
         if (co >= 6) continue;
-        const float v = out[r] + p.bh[co];
+        const float v = out[r];
         if (co < 2)
           p.seg[((size_t)n * 2 + co) * TH + pix] = v;
         else
