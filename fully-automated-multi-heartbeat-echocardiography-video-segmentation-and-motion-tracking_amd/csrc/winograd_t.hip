@@ -260,6 +260,8 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) vo
 // Each lane transforms its own (tile column, channel pair) from the raw frames into MFMA B operands
 // (no V round trip through LDS). A wave owns 2 tiles (adjacent in time: they share 2 of their 10
 // frames) x 64 channels: 96 MFMAs per chunk and barrier; 2 LDS stages, 2 blocks per CU.
+// TS = 1 (T = 4: one temporal tile, layer4 at 32-frame clips): a wave's 2 tiles are 2 column groups
+// of the single tile row instead (6 frames each), in the same accumulation order.
 template <int TS, int NT>
 struct T5 {
   static constexpr int P = 16 * 8 / TS;          // columns per block
@@ -337,12 +339,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   };
   // the lane's reads: raw frames of its tile column (m-tiles 2w, 2w+1 share a column group and are
   // adjacent in time), U fragments (co = 16 nt + l16, channel pair q)
+  constexpr bool COLS = TS == 1;  // the wave's 2 tiles side by side (column groups), not in time
   const int j0 = 2 * wid;
   const int c_rd = (j0 / TS) * 16 + l16;
   const int rd_off = (4 * (j0 % TS)) * (G::P * 8) + (c_rd * 2 + ((q >> 1) ^ ((c_rd >> 3) & 1))) * 4 + (q & 1) * 2;
+  const int c_rd1 = c_rd + 16;  // COLS: the second tile's column
+  const int rd_off1 = (c_rd1 * 2 + ((q >> 1) ^ ((c_rd1 >> 3) & 1))) * 4 + (q & 1) * 2;
   const int u_rd = G::RAW_I * 256 + (l16 * 2 + ((q >> 1) ^ ((l16 >> 3) & 1))) * 4 + (q & 1) * 2;  // floats
   const int t0w = t_seg + 4 * (j0 % TS);
-  const bool pad_lo = t0w == 0, pad_hi = t0w + 8 >= T;
+  const bool pad_lo = t0w == 0, pad_hi = t0w + (COLS ? 4 : 8) >= T;
 
   f32x4 acc[6][2][NT];
 #pragma unroll
@@ -362,18 +367,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (k + 1 < nchunk) issue(k + 1, (k + 1) & 1);
     __builtin_amdgcn_sched_barrier(0);
     const float* st = reinterpret_cast<const float*>(smem + (k & 1) * G::STAGE);
-    f32x2 d[10];
+    // frames of tile m: d[4m .. 4m + 5] (in time), or d[6m .. 6m + 5] (COLS: the m-th column group)
+    constexpr int ND = COLS ? 12 : 10, MS = COLS ? 6 : 4;
+    f32x2 d[ND];
 #pragma unroll
-    for (int f = 0; f < 10; ++f) d[f] = *reinterpret_cast<const f32x2*>(st + rd_off + f * (G::P * 8));
-    if (pad_lo) d[0] = f32x2{0.f, 0.f};
-    if (pad_hi) d[9] = f32x2{0.f, 0.f};
+    for (int f = 0; f < ND; ++f)
+      d[f] = *reinterpret_cast<const f32x2*>(st + (COLS && f >= 6 ? rd_off1 + (f - 6) * (G::P * 8) : rd_off + f * (G::P * 8)));
+    if (pad_lo) {
+      d[0] = f32x2{0.f, 0.f};
+      if constexpr (COLS) d[6] = f32x2{0.f, 0.f};
+    }
+    if (pad_hi) {
+      d[ND - 1] = f32x2{0.f, 0.f};
+      if constexpr (COLS) d[5] = f32x2{0.f, 0.f};
+    }
     f32x2 v[2][6];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        const float d0 = d[4 * m][s2], d1 = d[4 * m + 1][s2], d2 = d[4 * m + 2][s2], d3 = d[4 * m + 3][s2],
-                    d4 = d[4 * m + 4][s2], d5 = d[4 * m + 5][s2];
+        const float d0 = d[MS * m][s2], d1 = d[MS * m + 1][s2], d2 = d[MS * m + 2][s2], d3 = d[MS * m + 3][s2],
+                    d4 = d[MS * m + 4][s2], d5 = d[MS * m + 5][s2];
         const float e1 = d3 + d4, e2 = d1 + d2, e3 = d4 - d3, e4 = d1 - d2;
         v[m][0][s2] = 4.f * d0 - 5.f * d2 + d4;
         v[m][1][s2] = e1 - 4.f * e2;
@@ -401,13 +415,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float* res = reinterpret_cast<const float*>(p.res);
   float* yout = reinterpret_cast<float*>(p.y);
   const size_t fstride = (size_t)HW * CO;
-  const int gc = col0 + c_rd;
-  const bool ok = gc < n_cols;
-  const int gcc = ok ? gc : 0;
-  const int n = fdiv(gcc, fd_hw), pix = gcc - n * HW;
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    const int t0 = t0w + 4 * m;
+    const int gc = col0 + c_rd + (COLS ? 16 * m : 0);
+    const bool ok = gc < n_cols;
+    const int gcc = ok ? gc : 0;
+    const int n = fdiv(gcc, fd_hw), pix = gcc - n * HW;
+    const int t0 = t0w + (COLS ? 0 : 4 * m);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const int co = co0 + 16 * nt + 4 * q;
@@ -473,10 +487,11 @@ hipError_t winot5_launch(const ConvParams& p, hipStream_t s) {
 // 64 channels per wave (NT = 4); 32 when that leaves fewer than two blocks per CU (layer3 maps).
 hipError_t winot5_dispatch(const ConvParams& p, hipStream_t s, int force_nt = 0) {
   const int tt = p.Ti / 4;
-  const int ts = tt % 4 == 0 ? 4 : 2;
+  const int ts = tt % 4 == 0 ? 4 : tt % 2 == 0 ? 2 : 1;
   const long blocks64 = (long)((p.N * p.Hi * p.Wi + 16 * 8 / ts - 1) / (16 * 8 / ts)) * (tt / ts) * (p.Cout / 64);
   const int nt = force_nt ? force_nt : (blocks64 >= 512 ? 4 : 2);
   if (ts == 4) return nt == 4 ? winot5_launch<4, 4>(p, s) : winot5_launch<4, 2>(p, s);
+  if (ts == 1) return nt == 4 ? winot5_launch<1, 4>(p, s) : winot5_launch<1, 2>(p, s);
   return nt == 4 ? winot5_launch<2, 4>(p, s) : winot5_launch<2, 2>(p, s);
 }
 
@@ -487,6 +502,15 @@ bool winot5_fits(const ConvParams& p) { return (size_t)p.N * p.Ti * p.Hi * p.Wi 
 
 bool winot_c8_ok(const ConvParams& p) {
   return winot_supported(p) && getenv("CLASFV_WINOT_REFERENCE") == nullptr && p.Ti % 8 == 0 && winot5_fits(p);
+}
+
+// conv_winot5 for channels-last input: T % 8 == 0 in time-adjacent tile pairs, other T % 4 == 0 (one
+// tile row per segment) in column-adjacent pairs (TS = 1); CLASFV_WINOT_TS1=0 keeps the latter on
+// conv_winot
+static bool winot5_ok(const ConvParams& p) {
+  if (winot_c8_ok(p)) return true;
+  static const bool ts1 = [] { const char* e = getenv("CLASFV_WINOT_TS1"); return !(e && e[0] == '0'); }();
+  return ts1 && !p.x_c8 && winot_supported(p) && getenv("CLASFV_WINOT_REFERENCE") == nullptr && winot5_fits(p);
 }
 
 bool winot_supported(const ConvParams& p) {
@@ -500,9 +524,8 @@ bool winot_supported(const ConvParams& p) {
 hipError_t launch_winot(const ConvParams& p, hipStream_t s) {
   if (!winot_supported(p)) return hipErrorInvalidValue;
   // CLASFV_WINOT_REFERENCE=1 (tests): always conv_winot; both kernels compute the same products in
-  // the same order (bit-identical outputs). conv_winot5 needs T % 8 == 0 (whole tile pairs);
-  // layer4 at 32-frame clips (T = 4, fewer than 256 blocks) stays on conv_winot.
-  if (winot_c8_ok(p)) return winot5_dispatch(p, s);
+  // the same order (bit-identical outputs).
+  if (winot5_ok(p)) return winot5_dispatch(p, s);
   if (p.x_c8) return hipErrorInvalidValue;  // 8-channel-blocked input: conv_winot5 only
   static bool attr_set = false;
   if (!attr_set) {
