@@ -328,11 +328,14 @@ hipError_t launch_nt(const ConvParams& p, int nt, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-// N tile: the widest (fewest A re-reads, most MFMAs per LDS read) that still gives two blocks per
-// CU; the narrowest legal one when none does (layer4's 7x7 maps).
+// N tile: the widest (fewest A re-reads, most MFMAs per LDS read) that still gives about two
+// blocks per CU; the narrowest legal one when none does (layer4's 7x7 maps). 3x1x1 convs take the
+// wider tile from 448 blocks (profiles/r02h_convbench_patch_sweep.txt: layer3 temporal, 480 blocks
+// at NT = 8 vs 960 at NT = 4: 0.061 vs 0.069 ms).
 int patch_pick_nt(const ConvParams& p, int force_nt) {
   const int n16 = p.Cout / 16;
   const long base = patch_grid(p, p.KT == 1 ? product_fr<1>() : product_fr<3>()).base;
+  const long enough = p.KT == 3 ? 448 : 512;
   int pick = 0;
   for (int nt : {10, 9, 8, 6, 5, 4}) {
     if (n16 % nt) continue;
@@ -341,7 +344,7 @@ int patch_pick_nt(const ConvParams& p, int force_nt) {
       continue;
     }
     pick = nt;
-    if (base * (n16 / nt) >= 512) break;
+    if (base * (n16 / nt) >= enough) break;
   }
   return pick;
 }
