@@ -346,6 +346,18 @@ int patch_pick_nt(const ConvParams& p, int force_nt) {
     pick = nt;
     if (base * (n16 / nt) >= enough) break;
   }
+  // Small grids (under 3 resident blocks per CU): the busiest CU's share sets the time, so take the
+  // tile minimising ceil(blocks / 256) x (NT + 2) (the + 2: a block's fixed patch / epilogue cost in
+  // units of one 16-channel n tile). layer4 1x3x3 512 -> 1152 (convbench, 30 clips): NT 8 / 540
+  // blocks 0.094 ms, NT 9 / 480 0.082, NT 6 / 720 0.080.
+  if (force_nt <= 0 && pick && base * (n16 / pick) < 768) {
+    long best = -1;
+    for (int nt : {10, 9, 8, 6, 5, 4}) {
+      if (n16 % nt) continue;
+      const long cost = (base * (n16 / nt) + 255) / 256 * (nt + 2);
+      if (best < 0 || cost < best) best = cost, pick = nt;
+    }
+  }
   return pick;
 }
 
