@@ -43,21 +43,26 @@ GFLOP_PER_CLIP_C3 = 1340.68      # 64x224x224 clip, BASELINE.md §2
 FP32_PEAK_TFLOPS = 157.3         # MI355X fp32 (vector = MFMA), MI355X_MICROARCH.md
 BF16_PEAK_TFLOPS = 2500.0        # MI355X bf16 MFMA dense
 NORTHSTAR = os.path.join(REPO, "tests", "golden", "northstar_c1.npz")
+BENCH_WEIGHTS = "echo"           # seeded weights whose masks follow the synthetic LV (weights.echo_state_dict)
+DICE_BAR = {"fp32": 1e-3, "bf16": 1e-2}  # north_star: Dice within 1e-3 (fp32), 1e-2 (bf16/fp16)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU). Without WORLD_SIZE in the environment bench.py starts the N "
+                         "rank processes itself (torch.distributed.run on 127.0.0.1); under a launcher WORLD_SIZE "
+                         "must equal --gpus")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--videos-per-gpu", type=int, default=1)
     ap.add_argument("--frames", type=int, default=200)
-    ap.add_argument("--fuse", type=int, default=5)
+    ap.add_argument("--fuse", type=int, default=None, help="shifted passes per video (c1: 5, c2: 1)")
     ap.add_argument("--step", type=int, default=1)
     ap.add_argument("--fuse-method", default="simple")
     ap.add_argument("--batch-size", type=int, default=32, help="clips per forward call")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal, several ranks on one GPU)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"], help="encoder compute dtype of the headline run")
     ap.add_argument("--extra-bf16", type=int, default=1,
                     help="also time the bf16 path (BASELINE config[4]) on the same workload; reported as 'bf16'")
@@ -66,9 +71,53 @@ def parse():
     ap.add_argument("--c3-batch", type=int, default=8, help="64x224x224 clips per forward in the config3 run")
     ap.add_argument("--extra-stream", type=int, default=1,
                     help="also time the pipelined front end on host uint8 videos (PCIe-inclusive); reported as 'stream'")
-    ap.add_argument("--workload", default="c1", choices=["c1", "c3"],
-                    help="c1: config[1] fused video pipeline (headline); c3: only the config[3] forward")
-    return ap.parse_args()
+    ap.add_argument("--workload", default="c1", choices=["c1", "c2", "c3"],
+                    help="c1: config[1] fused video pipeline per GPU (headline, weak scaling); c2: config[2], a fixed "
+                         "batch of --c2-videos full videos sharded clip-wise over the ranks (strong scaling); "
+                         "c3: only the config[3] forward")
+    ap.add_argument("--c2-videos", type=int, default=64, help="videos in the config[2] batch")
+    ap.add_argument("--c2-extra-fuse", type=int, default=5,
+                    help="c2: also time the same batch with this many shifted passes (0: off); reported as 'fuse_extra'")
+    ap.add_argument("--master-port", type=int, default=0, help="rendezvous port of the self-launched ranks (0: free)")
+    args = ap.parse_args(argv)
+    if args.fuse is None:
+        args.fuse = 1 if args.workload == "c2" else 5
+    return args
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """--gpus N without WORLD_SIZE: start the N rank processes (torch.distributed.run, rendezvous on
+    127.0.0.1) and return their exit code. Runs before this process touches the GPU (no HIP call has
+    been made: device_count does not initialise it on this image), so only the children own devices."""
+    import subprocess
+    if args.dist_backend == "nccl" and torch.cuda.device_count() < args.gpus:
+        sys.exit(f"error: --gpus {args.gpus} with RCCL needs {args.gpus} visible GPUs "
+                 f"({torch.cuda.device_count()} visible); use --dist-backend gloo to rehearse on fewer")
+    port = args.master_port or free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, BENCH_SELF_LAUNCHED="1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def host_cpus():
+    """CPUs this process may use: its affinity mask, capped by a cgroup CPU quota when one is set (a
+    GPU box's share of the host is 16 CPUs while os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
 
 
 def timed(fn, steps, warmup, engine, world, dev):
@@ -148,7 +197,7 @@ def profiled_traffic(kernel, dtype):
     return {"bytes_per_launch": int((f + w) * 2**20 / max(n, 1)), "source": os.path.basename(files[-1])}
 
 
-def northstar_parity(args, fused_video0):
+def northstar_parity(args, fused_video0, dtype):
     """Dice delta (1 - Dice of the LV class, src/clasfv_losses.py:60-68) of this run's fused masks of
     video 0 and the |EF delta| (compute_ef_using_putative_clips, src/fuse_utils.py:105-148) against
     the CPU reference path on the same video, when the workload is the fixture's (config[1])."""
@@ -158,7 +207,8 @@ def northstar_parity(args, fused_video0):
         return None
     g = np.load(NORTHSTAR, allow_pickle=False)
     if (args.frames, args.fuse, args.step) != (int(g["T"]), int(g["fuse"]), int(g["step"])) or \
-            int(g["weights_seed"]) != W.DEFAULT_SEED or f"fused_{args.fuse_method}" not in g:
+            int(g["weights_seed"]) != W.DEFAULT_SEED or str(g["weights_recipe"]) != BENCH_WEIGHTS or \
+            f"fused_{args.fuse_method}" not in g:
         return None
     shp = tuple(g[f"fused_{args.fuse_method}_shape"])
     ref = np.unpackbits(g[f"fused_{args.fuse_method}"])[: int(np.prod(shp))].reshape(shp).astype(np.int64)
@@ -172,10 +222,12 @@ def northstar_parity(args, fused_video0):
         mean_delta = float(abs(np.nanmean(efs) - np.nanmean(ref_ef)))
     else:
         ef_delta = mean_delta = None
-    return {"dice_delta_fused_masks": round(float(1.0 - categorical_dice(got, ref, 1)), 9),
-            "ef_delta_max_per_systole": ef_delta, "ef_delta_mean": mean_delta, "ed_es_pairs_equal": same_pairs,
-            "efs_gpu": [round(float(e), 4) for e in efs], "reference": "tests/golden/northstar_c1.npz (oracle CPU "
-            "path, same video and weights, fuse=%s)" % args.fuse_method}
+    dice = float(1.0 - categorical_dice(got, ref, 1))
+    return {"dice_delta_fused_masks": round(dice, 9), "ef_delta_max_per_systole": ef_delta, "ef_delta_mean": mean_delta,
+            "ed_es_pairs_equal": same_pairs, "bar": DICE_BAR[dtype], "within_bar": dice <= DICE_BAR[dtype],
+            "efs_gpu": [round(float(e), 4) for e in efs], "efs_cpu": [round(float(e), 4) for e in ref_ef],
+            "reference": "tests/golden/northstar_c1.npz (oracle CPU path, same video and weights, fuse=%s)"
+                         % args.fuse_method}
 
 
 def cpu_baseline(args, S):
@@ -184,7 +236,7 @@ def cpu_baseline(args, S):
     plumbing + fusion of one whole video with the clip forwards replaced by cached logits."""
     from oracle import fuse_ref, r2plus1d_ref
     import clasfv_amd.weights as W
-    threads = min(os.cpu_count() or 1, 16)  # the GPU box's CPU share is 16 threads
+    threads = host_cpus()  # every CPU this process may use (affinity / cgroup quota)
     torch.set_num_threads(threads)
     model = r2plus1d_ref.OracleModel(W.synthetic_state_dict())
     v = fuse_ref.zeroone_normalizer(S.echo_video(args.frames, seed=0))
@@ -212,9 +264,24 @@ def cpu_baseline(args, S):
                       f"{n_total} clips of one step"}
 
 
+def gather_ranks(obj, world):
+    """Every rank's `obj` on every rank (list in rank order)."""
+    if world == 1:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args))
+    elif int(env_world) != args.gpus:
+        sys.exit(f"error: WORLD_SIZE={env_world} (launcher) but --gpus {args.gpus}: they must agree")
+    world = int(env_world or 1)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
@@ -225,60 +292,136 @@ def main():
         else:  # rehearsal of the exchange with several ranks on one GPU
             dist.init_process_group(args.dist_backend)
 
-    import clasfv_amd.synthetic as S
-    from clasfv_amd import dist as D
     from clasfv_amd.model import R2plus1D_18_MotionNet
+    model = R2plus1D_18_MotionNet(pretrained=False, dtype=args.dtype, device=dev, weights=BENCH_WEIGHTS)
+    run = {"c1": run_c1, "c2": run_c2, "c3": run_c3_only}[args.workload]
+    line = run(args, model, world, rank, dev)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def c3_run(args, model, world, dev, steps, warmup):
+    import clasfv_amd.synthetic as S
     from clasfv_amd.preprocess import zeroone_normalize_
-
-    model = R2plus1D_18_MotionNet(pretrained=False, dtype=args.dtype, device=dev)
     eng = model.engine
+    x = torch.cat([zeroone_normalize_(torch.from_numpy(S.echo_video(64, H=224, W=224, seed=21 + i)).to(dev))[None]
+                   for i in range(args.c3_batch)])
+    dt, kt, _ = timed(lambda: model(x), steps, warmup, eng, world, dev)
+    n = args.c3_batch * steps * world
+    peak = BF16_PEAK_TFLOPS if eng.dtype == "bf16" else FP32_PEAK_TFLOPS
+    return {"value": round(n / dt, 3), "unit": "64x224x224 clips/s", "ms_per_step": round(dt / steps * 1e3, 3),
+            "clips_per_step": args.c3_batch * world,
+            "forward": forward_stats(kt, args.c3_batch * steps, GFLOP_PER_CLIP_C3, peak),
+            "roofline": kernel_roofline(kt, peak, eng.dtype + "_c3"),  # no c3 PMC profile: traffic null
+            "note": "BASELINE config[3]: (N,3,64,224,224) model forward (seg + motion), the reference's "
+                    "forward signature; the CLI path is fixed at 112x112 (src/fuse_utils.py:22)"}
 
-    def c3_run(steps, warmup):
-        x = torch.cat([zeroone_normalize_(torch.from_numpy(S.echo_video(64, H=224, W=224, seed=21 + i)).to(dev))[None]
-                       for i in range(args.c3_batch)])
-        dt, kt, _ = timed(lambda: model(x), steps, warmup, eng, world, dev)
-        n = args.c3_batch * steps * world
-        peak = BF16_PEAK_TFLOPS if model.engine.dtype == "bf16" else FP32_PEAK_TFLOPS
-        return {"value": round(n / dt, 3), "unit": "64x224x224 clips/s", "ms_per_step": round(dt / steps * 1e3, 3),
-                "clips_per_step": args.c3_batch * world, "forward": forward_stats(kt, args.c3_batch * steps,
-                                                                                 GFLOP_PER_CLIP_C3, peak),
-                "roofline": kernel_roofline(kt, peak, model.engine.dtype + "_c3"),  # no c3 PMC profile: traffic null
-                "note": "BASELINE config[3]: (N,3,64,224,224) model forward (seg + motion), the reference's "
-                        "forward signature; the CLI path is fixed at 112x112 (src/fuse_utils.py:22)"}
 
-    if args.workload == "c3":
-        res = c3_run(args.steps, args.warmup)
-        if rank == 0:
-            print(json.dumps({"metric": "64f×224×224 clips/sec (BASELINE config[3])", "value": res["value"],
-                              "unit": res["unit"], "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                              "ms_per_step": res["ms_per_step"], "higher_is_better": True, "scaling": "weak",
-                              "vs_baseline": None, "dtype": model.engine.dtype, "data": "synthetic",
-                              "config": {"workload": "BASELINE config[3]: 64-frame 224x224 clips, model forward",
-                                         "batch": args.c3_batch},
-                              "roofline": res["roofline"], "forward": res["forward"]}), flush=True)
-        if world > 1:
-            dist.destroy_process_group()
-        return
+def run_c3_only(args, model, world, rank, dev):
+    res = c3_run(args, model, world, dev, args.steps, args.warmup)
+    return {"metric": "64f×224×224 clips/sec (BASELINE config[3])", "value": res["value"], "unit": res["unit"],
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": model.engine.dtype,
+            "data": "synthetic", "config": {"workload": "BASELINE config[3]: 64-frame 224x224 clips, model forward",
+                                            "batch": args.c3_batch},
+            "roofline": res["roofline"], "forward": res["forward"]}
 
+
+def make_videos(args, lengths, needed, dev):
+    """Synthetic EchoNet-style videos (seed = video index), normalised on the device; None for the
+    videos this rank does not hold (not timed)."""
+    import clasfv_amd.synthetic as S
+    from clasfv_amd.preprocess import zeroone_normalize_
+    out = [None] * len(lengths)
+    for v in needed:
+        x = torch.from_numpy(S.echo_video(lengths[v], seed=v)).to(dev)
+        out[v] = zeroone_normalize_(x.contiguous())
+    return out
+
+
+def run_c2(args, model, world, rank, dev):
+    """BASELINE config[2]: a fixed batch of full videos (64 x 200 frames) sharded clip-wise over the
+    ranks (strong scaling). f = 1: 384 clips; the fuse_extra run repeats it with f = 5 (1920 clips)."""
+    from clasfv_amd import dist as D
+    eng = model.engine
+    lengths = [args.frames] * args.c2_videos
+    peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else FP32_PEAK_TFLOPS
+
+    def one(fuse, steps, warmup):
+        needed = D.videos_needed(lengths, fuse, args.step, rank, world)
+        videos = make_videos(args, lengths, needed, dev)
+        plans, n_total = D.global_clip_plan(lengths, fuse, args.step)
+        lo, hi = D.shard_bounds(n_total, rank, world)
+
+        def step():
+            return D.segment_videos_sharded(videos, model, num_clips=fuse, step=args.step,
+                                            fuse_method=args.fuse_method, rank=rank, world=world,
+                                            batch_size=args.batch_size, lengths=lengths)
+
+        dt, kt, out = timed(step, steps, warmup, eng, world, dev)
+        fwd = forward_stats(kt, (hi - lo) * steps, GFLOP_PER_CLIP, peak)
+        rows, nbytes = D.exchange_stats(lengths, fuse, args.step, world)
+        mine = {"rank": rank, "clips": hi - lo, "videos_held": len(needed), "videos_fused": len(out),
+                "forward_ms_per_step": round(sum(v["ms"] for v in kt.values()) / steps, 3)}
+        per_rank = gather_ranks(mine, world)
+        del videos
+        torch.cuda.empty_cache()
+        return {"value": round(n_total * steps / dt, 3), "unit": "clips/s", "ms_per_step": round(dt / steps * 1e3, 3),
+                "clips_per_step": n_total, "fuse": fuse, "forward": fwd, "per_rank": per_rank,
+                "rows_exchanged_per_step": rows, "bytes_exchanged_per_step": nbytes,
+                "roofline": kernel_roofline(kt, peak, args.dtype), "kt": kt, "out": out}
+
+    main_run = one(args.fuse, args.steps, args.warmup)
+    extra = None
+    if args.c2_extra_fuse and args.c2_extra_fuse != args.fuse:
+        extra = one(args.c2_extra_fuse, max(2, args.steps // 3), 1)
+        extra = {k: v for k, v in extra.items() if k not in ("kt", "out")}
+    lv = [float(o.float().mean().item()) for o in main_run["out"].values()]
+    lv_all = gather_ranks(lv, world)
+    return {
+        "metric": METRIC, "value": main_run["value"], "unit": "clips/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": main_run["ms_per_step"], "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic EchoNet-style videos (seeded), seeded synthetic weights (" + BENCH_WEIGHTS + " recipe)",
+        "config": {"workload": f"BASELINE config[2]: batch of {args.c2_videos} videos x {args.frames} frames, "
+                               f"{args.fuse} shifted pass(es), clips sharded over {world} rank(s) + per-frame "
+                               f"{args.fuse_method} fusion on each video's owner",
+                   "videos": args.c2_videos, "frames": args.frames, "fuse": args.fuse, "step": args.step,
+                   "clips_per_step": main_run["clips_per_step"], "batch_size": args.batch_size,
+                   "parallelism": f"clip-shard x{world} ({args.dist_backend}); owner all_to_all of logit margins "
+                                  f"only for straddling videos"},
+        "roofline": main_run["roofline"], "forward": main_run["forward"], "per_rank": main_run["per_rank"],
+        "rows_exchanged_per_step": main_run["rows_exchanged_per_step"],
+        "bytes_exchanged_per_step": main_run["bytes_exchanged_per_step"],
+        "fuse_extra": extra, "lv_fraction": round(float(np.mean(sum(lv_all, []))), 4),
+    }
+
+
+def run_c1(args, model, world, rank, dev):
+    """BASELINE config[1] per GPU (the headline): each rank fuses its own 200-frame video(s) with 5
+    shifted passes (weak scaling)."""
+    from clasfv_amd import dist as D
+    eng = model.engine
     n_videos = args.videos_per_gpu * world
-    videos = []
-    for v in range(n_videos):  # synthetic EchoNet-style videos, normalised on the device (not timed)
-        x = torch.from_numpy(S.echo_video(args.frames, seed=v)).to(dev)
-        videos.append(zeroone_normalize_(x.contiguous()))
-    plans, n_total = D.global_clip_plan([v.shape[1] for v in videos], args.fuse, args.step)
+    lengths = [args.frames] * n_videos
+    needed = D.videos_needed(lengths, args.fuse, args.step, rank, world)
+    videos = make_videos(args, lengths, needed, dev)
+    plans, n_total = D.global_clip_plan(lengths, args.fuse, args.step)
     lo, hi = D.shard_bounds(n_total, rank, world)
 
     def step():
         return D.segment_videos_sharded(videos, model, num_clips=args.fuse, step=args.step,
                                         fuse_method=args.fuse_method, rank=rank, world=world,
-                                        batch_size=args.batch_size)
+                                        batch_size=args.batch_size, lengths=lengths)
 
     dt, ktimes, out = timed(step, args.steps, args.warmup, eng, world, dev)
     value = n_total * args.steps / dt
     peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else FP32_PEAK_TFLOPS
     fwd = forward_stats(ktimes, (hi - lo) * args.steps, GFLOP_PER_CLIP, peak)
     lv_frac = float(np.mean([o.float().mean().item() for o in out.values()])) if out else 0.0
-    parity = northstar_parity(args, out[0]) if (0 in out and args.dtype == "fp32") else None
+    parity = northstar_parity(args, out[0], args.dtype) if 0 in out else None
 
     bf16 = None
     if args.extra_bf16 and args.dtype == "fp32":
@@ -291,15 +434,17 @@ def main():
                 "ms_per_step": round(dt16 / args.steps * 1e3, 3),
                 "forward": forward_stats(k16, (hi - lo) * args.steps, GFLOP_PER_CLIP, BF16_PEAK_TFLOPS),
                 "dice_delta_vs_fp32_fused_masks": round(float(max(d16)) if d16 else 0.0, 6),
+                "parity_vs_cpu": northstar_parity(args, out16[0], "bf16") if 0 in out16 else None,
                 "roofline": kernel_roofline(k16, BF16_PEAK_TFLOPS, "bf16"),
                 "note": "BASELINE config[4]: bf16 activations/weights, fp32 accumulate, fp32 decoder head; "
                         "Dice tolerance 1e-2"}
         model.set_compute_dtype("fp32")
 
-    c3 = c3_run(max(2, args.steps // 2), 1) if args.extra_c3 else None
+    c3 = c3_run(args, model, world, dev, max(2, args.steps // 2), 1) if args.extra_c3 else None
 
     stream = None
     if args.extra_stream and world == 1:
+        import clasfv_amd.synthetic as S
         from clasfv_amd.stream import VideoStream
         hv = [S.echo_video_uint8(args.frames, seed=v) for v in range(8)]
         vs = VideoStream(model, num_clips=args.fuse, step=args.step, fuse_method=args.fuse_method,
@@ -317,46 +462,43 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
+        import clasfv_amd.synthetic as S
         cpu = cpu_baseline(args, S)
 
-    if rank == 0:
-        line = {
-            "metric": METRIC,
-            "value": round(value, 3),
-            "unit": "clips/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": args.dtype,
-            "data": "synthetic EchoNet-style video (seeded), seeded synthetic weights",
-            "config": {"workload": "BASELINE config[1] per GPU: 200-frame 112x112 video, 5 shifted passes "
-                                   "(30 x 32-frame clips) + per-frame SIMPLE label fusion",
-                       "videos_per_gpu": args.videos_per_gpu, "frames": args.frames, "fuse": args.fuse,
-                       "step": args.step, "clips_per_step": n_total, "batch_size": args.batch_size,
-                       "parallelism": f"clip-shard x{world}; videos fused on the rank holding their clips "
-                                      f"(owner all_to_all of logit margins only for straddling videos)"},
-            "roofline": kernel_roofline(ktimes, peak, args.dtype),
-            "forward": fwd,
-            "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
-                            "issued_tflops": round(v["xgflop"] / max(v["ms"], 1e-9), 2),
-                            "algorithmic_tflops": round(v["gflop"] / max(v["ms"], 1e-9), 2)}
-                        for k, v in ktimes.items()},
-            "cpu_baseline": cpu,
-            "dice_delta_vs_cpu": parity and parity["dice_delta_fused_masks"],
-            "ef_delta_vs_cpu": parity and parity["ef_delta_max_per_systole"],
-            "parity": parity,
-            "bf16": bf16,
-            "config3": c3,
-            "stream": stream,
-            "lv_fraction": round(lv_frac, 4),
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    return {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "clips/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic EchoNet-style video (seeded), seeded synthetic weights (" + BENCH_WEIGHTS + " recipe)",
+        "config": {"workload": "BASELINE config[1] per GPU: 200-frame 112x112 video, 5 shifted passes "
+                               "(30 x 32-frame clips) + per-frame SIMPLE label fusion",
+                   "videos_per_gpu": args.videos_per_gpu, "frames": args.frames, "fuse": args.fuse,
+                   "step": args.step, "clips_per_step": n_total, "batch_size": args.batch_size,
+                   "parallelism": f"clip-shard x{world}; videos fused on the rank holding their clips "
+                                  f"(owner all_to_all of logit margins only for straddling videos)"},
+        "roofline": kernel_roofline(ktimes, peak, args.dtype),
+        "forward": fwd,
+        "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                        "issued_tflops": round(v["xgflop"] / max(v["ms"], 1e-9), 2),
+                        "algorithmic_tflops": round(v["gflop"] / max(v["ms"], 1e-9), 2)}
+                    for k, v in ktimes.items()},
+        "cpu_baseline": cpu,
+        "dice_delta_vs_cpu": parity and parity["dice_delta_fused_masks"],
+        "ef_delta_vs_cpu": parity and parity["ef_delta_max_per_systole"],
+        "parity": parity,
+        "bf16": bf16,
+        "config3": c3,
+        "stream": stream,
+        "lv_fraction": round(lv_frac, 4),
+    }
 
 
 if __name__ == "__main__":

@@ -24,6 +24,8 @@ SIGNATURES = {
     "clasfv_workspace_bytes": (c_int64, [_P]),
     "clasfv_set_compute_dtype": (c_int, [_P, c_int]),
     "clasfv_get_compute_dtype": (c_int, [_P]),
+    "clasfv_set_kernel_variants": (c_int, [_P, c_int]),
+    "clasfv_get_kernel_variants": (c_int, [_P]),
     "clasfv_set_kernel_timing": (c_int, [_P, c_int]),
     "clasfv_kernel_timing": (c_int, [_P, c_int, ctypes.POINTER(c_char_p), ctypes.POINTER(c_int),
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
@@ -40,7 +42,12 @@ SIGNATURES = {
     "clasfv_preprocess_video": (c_int, [_P, c_int, c_int, c_int, c_int, c_int, _P, _P]),
 }
 
-FUSE_MAJORITY, FUSE_SIMPLE, FUSE_STAPLE = 0, 1, 2
+ABI_VERSION = 3  # CLASFV_ABI_VERSION of include/clasfv.h these signatures describe
+FUSE_MAJORITY, FUSE_SIMPLE, FUSE_STAPLE, FUSE_ITKVOTING = 0, 1, 2, 3
+FUSE_FORCE_GENERIC = 0x100
+# CLASFV_VARIANT_* bits (include/clasfv.h)
+VARIANTS = {"no_winograd": 1, "no_wino_patch": 2, "winot_reference": 4, "no_c8": 8, "no_stem_bf16": 16,
+            "no_patch_bf16": 32, "no_decoder_bf16": 64, "winot_no_ts1": 128}
 DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
 _lib = None
 
@@ -62,6 +69,9 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.clasfv_version() != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: ABI version {lib.clasfv_version()}, expected {ABI_VERSION}: rebuild it "
+                           f"(python -m clasfv_amd.build --force)")
     _lib = lib
     return lib
 

@@ -13,7 +13,8 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 INCLUDE = os.path.join(REPO_DIR, "include")
 LIB_PATH = os.path.join(PKG_DIR, "libclasfv.so")
-SOURCES = ["engine.hip", "conv.hip", "conv_patch.hip", "winograd.hip", "winograd2.hip", "winograd3.hip", "winograd_t.hip", "winograd_w.hip", "decoder.hip", "plumbing.hip"]
+SOURCES = ["engine.hip", "conv.hip", "conv_patch.hip", "winograd.hip", "winograd2.hip", "winograd_t.hip", "decoder.hip",
+           "plumbing.hip"]
 HEADERS = ["common.h", "plumbing.h"]
 ARCH = os.environ.get("CLASFV_OFFLOAD_ARCH", "gfx950")
 # Per-file extra flags. winograd_t.hip: no SLP vectorisation -- packed f32 VALU (v_pk_*) beside
@@ -44,12 +45,26 @@ def up_to_date():
 def build(force=False, verbose=False):
     """Compile the engine. Returns the library path. Each source is compiled to an object in
     parallel (every kernel is launched from its own translation unit, so no relocatable device
-    code is needed), then the objects are linked into one shared library."""
+    code is needed), then the objects are linked into one shared library.
+
+    Concurrent callers (e.g. every rank of a torchrun job finding no library) are serialised by an
+    exclusive lock on build.lock; each build compiles into its own temporary directory and the
+    finished library replaces the old one atomically."""
     if not force and up_to_date():
         return LIB_PATH
+    import fcntl
+    with open(os.path.join(PKG_DIR, "build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        if not force and up_to_date():  # another process built it while this one waited
+            return LIB_PATH
+        return _build_locked(verbose)
+
+
+def _build_locked(verbose):
+    import tempfile
     from concurrent.futures import ThreadPoolExecutor
-    objdir = os.path.join(PKG_DIR, "build_obj")
-    os.makedirs(objdir, exist_ok=True)
+    os.makedirs(os.path.join(PKG_DIR, "build_obj"), exist_ok=True)
+    objdir = tempfile.mkdtemp(prefix="build-", dir=os.path.join(PKG_DIR, "build_obj"))
     hipcc = _hipcc()
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", INCLUDE]
 
@@ -64,14 +79,17 @@ def build(force=False, verbose=False):
         return obj
 
     jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
-    with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(compile_one, SOURCES))
-    tmp = LIB_PATH + ".tmp"
-    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs,
-                       capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"link failed ({r.returncode}):\n{r.stderr[-6000:]}")
-    os.replace(tmp, LIB_PATH)
+    try:
+        with ThreadPoolExecutor(jobs) as ex:
+            objs = list(ex.map(compile_one, SOURCES))
+        tmp = os.path.join(objdir, "libclasfv.so")
+        r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs,
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed ({r.returncode}):\n{r.stderr[-6000:]}")
+        os.replace(tmp, LIB_PATH)
+    finally:
+        shutil.rmtree(objdir, ignore_errors=True)
     return LIB_PATH
 
 

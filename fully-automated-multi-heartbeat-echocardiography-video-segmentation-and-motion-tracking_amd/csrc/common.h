@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "clasfv.h"
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // n / d for a runtime divisor d >= 1 and n < 2^31 as one multiply-high and an add (Granlund-Montgomery
@@ -44,6 +46,10 @@ struct ConvParams {
   // patches and conv_stem_f32 write y_c8) and the temporal Winograd consumer (conv_winot5 reads x_c8), whose
   // 8-channel chunks then read whole 128-B lines instead of 32 B of every pixel.
   int x_c8, y_c8;
+  // Kernel-choice switches of the engine (CLASFV_VARIANT_* of include/clasfv.h, read from the
+  // environment once at clasfv_create or set with clasfv_set_kernel_variants) and the tuning
+  // overrides of the bf16 patch kernel's N tile (0: automatic).
+  int vflags, patch_nt;
 };
 
 // Decoder tap: low-resolution projection P_i = (s1 * W_i) . f_i, channels-last with 64 channels.
@@ -78,15 +84,6 @@ void wino_transform_weights(const double* w, int cout, int cin, int cout_p, int 
 // Patch-tiled Winograd F(2x2,3x3) for Ho, Wo % 4 == 0 (winograd2.hip); p.w = conv_wino's U.
 bool winoq_supported(const ConvParams& p);
 hipError_t launch_winoq(const ConvParams& p, hipStream_t s);
-// Barrier-free patch-tiled Winograd F(2x2,3x3) (winograd_w.hip): the conv_wino_q op on 8x8-pixel
-// patches for Cin 64 / 128, bit-identical to it; p.w = conv_wino's U.
-bool winow_supported(const ConvParams& p);
-hipError_t launch_winow(const ConvParams& p, hipStream_t s);
-// Patch-tiled Winograd F(2x4,3x3) (winograd3.hip), Ho, Wo % 8 == 0; p.w = U below.
-bool winor_supported(const ConvParams& p);
-hipError_t launch_winor(const ConvParams& p, hipStream_t s);
-// U[cin_p/8][4][cout_p][4][6][2] from folded weights w[cout][cin][3][3] (double).
-void winor_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 // Fused Winograd F(4,3)-in-time path for stride-1 3x1x1 fp32 convs; p.w = transformed weights.
 bool winot_supported(const ConvParams& p);
 hipError_t launch_winot(const ConvParams& p, hipStream_t s);

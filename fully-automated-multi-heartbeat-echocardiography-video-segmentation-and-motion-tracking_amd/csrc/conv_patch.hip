@@ -379,8 +379,7 @@ bool patch_bf16_supported(const ConvParams& p) {
 
 hipError_t launch_patch_bf16(const ConvParams& p, hipStream_t s) {
   if (!patch_bf16_supported(p)) return hipErrorInvalidValue;
-  static const int force_nt = getenv("CLASFV_PATCH_NT") ? atoi(getenv("CLASFV_PATCH_NT")) : 0;  // A/B
-  const int nt = patch_pick_nt(p, force_nt);
+  const int nt = patch_pick_nt(p, p.patch_nt);
   return p.KT == 1 ? launch_nt<1>(p, nt, s) : launch_nt<3>(p, nt, s);
 }
 

@@ -78,31 +78,45 @@ struct Conv {
   void* dw = nullptr;     // weights, dtype of the conv's input
   float* db = nullptr;    // folded-BN bias (fp32)
   float* dwino = nullptr;  // Winograd F(2x2,3x3) transformed weights (fp32 stride-1 1x3x3 convs)
-  float* dwinor = nullptr;  // Winograd F(2x4,3x3) transformed weights (the same convs, Cin <= 128)
   float* dwinot = nullptr;  // Winograd F(4,3)-in-time transformed weights (fp32 stride-1 3x1x1 convs)
   void* dws16 = nullptr;    // bf16 stem weights, hi and lo images [64][7 kh][8 kw][4 c] (bf16 engines)
 };
 
-// fp32 stride-1 1x3x3 convs run on the fused Winograd kernel unless CLASFV_WINOGRAD=0.
-// fp32 stride-1 3x1x1 convs run on the fused temporal Winograd kernel unless CLASFV_WINOGRAD=0.
-bool use_winot(const Conv& c, bool bf16) {
-  const char* e = getenv("CLASFV_WINOGRAD");
-  if (e && e[0] == '0') return false;
+// fp32 stride-1 3x1x1 convs run on the fused temporal Winograd kernel, fp32 stride-1 1x3x3 convs on
+// the fused spatial one (CLASFV_VARIANT_NO_WINOGRAD: both on the direct implicit GEMM).
+bool use_winot(const Conv& c, bool bf16, int vflags) {
+  if (vflags & CLASFV_VARIANT_NO_WINOGRAD) return false;
   return !bf16 && (c.role == STEM_T || c.role == TP1 || c.role == TP2) && c.kt == 3 && c.kh == 1 && c.kw == 1 &&
          c.st == 1 && c.cin_p % 8 == 0 && c.cout_p % 64 == 0;
 }
 
-bool use_winor(const Conv& c, bool bf16);
-
-bool use_wino(const Conv& c, bool bf16) {
-  const char* e = getenv("CLASFV_WINOGRAD");
-  if (e && e[0] == '0') return false;
+bool use_wino(const Conv& c, bool bf16, int vflags) {
+  if (vflags & CLASFV_VARIANT_NO_WINOGRAD) return false;
   return !bf16 && (c.role == SP1 || c.role == SP2) && c.kt == 1 && c.kh == 3 && c.kw == 3 && c.sh == 1 &&
          c.sw == 1 && c.cin_p % 16 == 0 && c.cout_p % 48 == 0;
 }
 
-// F(2x4,3x3) weights only where conv_wino_r can run at 112x112 / 224x224 clips (layer1, layer2).
-bool use_winor(const Conv& c, bool bf16) { return use_wino(c, bf16) && c.cin_p <= 128; }
+// Kernel-variant flags and tuning overrides from the environment (read once, at clasfv_create).
+int env_variants() {
+  auto on = [](const char* n) { return getenv(n) != nullptr; };
+  const char* w = getenv("CLASFV_WINOGRAD");
+  const char* ts1 = getenv("CLASFV_WINOT_TS1");
+  int f = 0;
+  if (w && w[0] == '0') f |= CLASFV_VARIANT_NO_WINOGRAD;
+  if (on("CLASFV_NO_WINO_PATCH")) f |= CLASFV_VARIANT_NO_WINO_PATCH;
+  if (on("CLASFV_WINOT_REFERENCE")) f |= CLASFV_VARIANT_WINOT_REFERENCE;
+  if (on("CLASFV_NO_C8")) f |= CLASFV_VARIANT_NO_C8;
+  if (on("CLASFV_NO_STEM_BF16")) f |= CLASFV_VARIANT_NO_STEM_BF16;
+  if (on("CLASFV_NO_PATCH_BF16")) f |= CLASFV_VARIANT_NO_PATCH_BF16;
+  if (on("CLASFV_NO_DECODER_BF16")) f |= CLASFV_VARIANT_NO_DECODER_BF16;
+  if (ts1 && ts1[0] == '0') f |= CLASFV_VARIANT_WINOT_NO_TS1;
+  return f;
+}
+
+int env_int(const char* name) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : 0;
+}
 
 // Channel padding, K extent and dtypes of one conv for the engine's compute dtype.
 void layout_conv(Conv& c, bool bf16) {
@@ -131,6 +145,12 @@ Conv make_conv(Role role, const std::string& w, const std::string& bn, int cin, 
 
 int midplanes(int i, int o) { return (i * o * 27) / (i * 9 + 3 * o); }
 
+// Engine-wide kernel switches: CLASFV_VARIANT_* flags and the implicit-GEMM / patch-kernel tile
+// overrides (0: automatic).
+struct Tuning {
+  int vflags = 0, conv_nt = 0, conv_mt = 0, patch_nt = 0;
+};
+
 }  // namespace
 
 struct clasfv_engine {
@@ -142,6 +162,7 @@ struct clasfv_engine {
   float *b1 = nullptr, *w2 = nullptr, *b2 = nullptr, *wh = nullptr, *bh = nullptr;
   bool ready = false;
   int dtype = CLASFV_DTYPE_FP32;  // compute dtype of the encoder convs
+  Tuning tune;                    // kernel variants / tile overrides (environment at create)
   // workspace arena
   char* arena = nullptr;
   size_t arena_bytes = 0;
@@ -300,9 +321,8 @@ double conv_gflop(const Conv& c, const Shape5& out) {
 double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
   const double nt = (double)out.n * out.t;
   const double cc = (double)c.cin_p * c.cout_p;
-  if (!strcmp(kname, "conv_wino_q") || !strcmp(kname, "conv_wino_w") || !strcmp(kname, "conv_wino"))
+  if (!strcmp(kname, "conv_wino_q") || !strcmp(kname, "conv_wino"))
     return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 1) / 2) * 16.0 * cc * 1e-9;
-  if (!strcmp(kname, "conv_wino_r")) return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 3) / 4) * 24.0 * cc * 1e-9;
   if (!strcmp(kname, "conv_winot")) return 2.0 * out.n * (out.t / 4) * (double)out.h * out.w * 6.0 * cc * 1e-9;
   if (!strcmp(kname, "conv_stem_bf16"))
     return 3 * 2.0 * ceil((double)out.n * out.t * out.h * out.w / 256.0) * 256.0 * 64.0 * 224.0 * 1e-9;
@@ -338,50 +358,45 @@ ConvParams conv_params(const Conv& c, const Shape5& in, Shape5& out) {
   return p;
 }
 
-// The kernel run_conv launches for c with parameters p (the A/B switches are read here).
+// The kernel run_conv launches for c with parameters p (p.vflags selects A/B variants).
 const char* pick_kernel(const Conv& c, ConvParams p) {
-  // F(2x4,3x3) is opt-in: 25 % fewer MFMAs than conv_wino_q but 1.5x its U operand traffic per
-  // output; measured slower on layer1 (2.80 vs 2.40 ms)
-  if (c.dwinor && getenv("CLASFV_WINO_R") && winor_supported(p)) return "conv_wino_r";
   if (c.dwino) {
-    const bool no_patch = getenv("CLASFV_NO_WINO_PATCH") != nullptr;  // A/B switch (tests)
-    // conv_wino_w (barrier-free, bit-identical) is opt-in: measured 2.89 vs 2.31 ms per layer1 launch
-    // (4x the LDS-DMA instructions, paired 32-bank LDS reads, and the compiler drains every LDS-DMA in
-    // flight before the first chunks' reads)
-    if (!no_patch && getenv("CLASFV_WINO_W") && winow_supported(p)) return "conv_wino_w";
+    const bool no_patch = (p.vflags & CLASFV_VARIANT_NO_WINO_PATCH) != 0;
     if (!no_patch && winoq_supported(p)) return "conv_wino_q";
     if (wino_supported(p)) return "conv_wino";
   }
-  static const bool no_stem_bf16 = getenv("CLASFV_NO_STEM_BF16") != nullptr;  // A/B switch (tests)
-  if (c.dws16 && !no_stem_bf16 && stem_bf16_supported(p)) return "conv_stem_bf16";
+  if (c.dws16 && !(p.vflags & CLASFV_VARIANT_NO_STEM_BF16) && stem_bf16_supported(p)) return "conv_stem_bf16";
   if (c.dwinot && winot_supported(p)) return "conv_winot";
-  const bool no_patch_bf16 = getenv("CLASFV_NO_PATCH_BF16") != nullptr;  // A/B switch (tests)
-  if (!no_patch_bf16 && patch_bf16_supported(p)) return "conv_patch_bf16";
+  if (!(p.vflags & CLASFV_VARIANT_NO_PATCH_BF16) && patch_bf16_supported(p)) return "conv_patch_bf16";
   return c.stem ? "conv_stem_f32" : "conv_dma";
 }
 
 // Whether the mid tensor between producer `a` (input shape `in`) and consumer `b` goes through HBM
 // in the 8-channel-blocked layout: `a` runs on a kernel that writes it and `b` on conv_winot5,
-// which reads it (CLASFV_NO_C8=1: always channels-last, A/B switch).
-bool c8_pair(const Conv& a, const Conv& b, const Shape5& in) {
-  if (getenv("CLASFV_NO_C8")) return false;
+// which reads it (CLASFV_VARIANT_NO_C8: always channels-last).
+bool c8_pair(const Conv& a, const Conv& b, const Shape5& in, const Tuning& tu) {
+  if (tu.vflags & CLASFV_VARIANT_NO_C8) return false;
   Shape5 mid, out;
   ConvParams pa = conv_params(a, in, mid);
   ConvParams pb = conv_params(b, mid, out);
   pa.w = a.dwino ? (const void*)a.dwino : a.dw;
   pb.w = b.dwinot;
+  pa.vflags = pb.vflags = tu.vflags;
   const char* ka = pick_kernel(a, pa);
   // Measured per producer (30 clips, profiles/r02j_*): stem and conv_wino_q (layer1, layer2) write
   // the blocked layout at no cost while the temporal kernels after them gain 7-24 %; conv_wino
   // (layer3) broke even and stays channels-last.
-  const bool writes = !strcmp(ka, "conv_wino_q") || !strcmp(ka, "conv_wino_w") || !strcmp(ka, "conv_stem_f32");
+  const bool writes = !strcmp(ka, "conv_wino_q") || !strcmp(ka, "conv_stem_f32");
   return writes && !a.out_bf16 && !strcmp(pick_kernel(b, pb), "conv_winot") && winot_c8_ok(pb);
 }
 
 int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
-             hipStream_t s, const void* zero_block, const void* x2, const char** kname, int x_c8 = 0, int y_c8 = 0) {
+             hipStream_t s, const void* zero_block, const void* x2, const char** kname, const Tuning& tu, int x_c8 = 0,
+             int y_c8 = 0) {
   if (in.c != c.cin_p) return fail(CLASFV_EINVAL, "internal: channel mismatch");
   ConvParams p = conv_params(c, in, out);
+  p.vflags = tu.vflags;
+  p.patch_nt = tu.patch_nt;
   p.x = x;
   p.res = res;
   p.y = y;
@@ -392,16 +407,10 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   p.y_c8 = y_c8;
   const char* k = pick_kernel(c, p);
   *kname = k;
-  const bool c8_out = !strcmp(k, "conv_wino_q") || !strcmp(k, "conv_wino_w") || !strcmp(k, "conv_stem_f32");
+  const bool c8_out = !strcmp(k, "conv_wino_q") || !strcmp(k, "conv_stem_f32");
   if ((y_c8 && !c8_out) || (x_c8 && strcmp(k, "conv_winot")))
     return fail(CLASFV_EINVAL, "internal: 8-channel-blocked layout on an unsupported kernel");
-  if (!strcmp(k, "conv_wino_r")) {
-    p.w = c.dwinor;
-    HIP_TRY(launch_winor(p, s));
-  } else if (!strcmp(k, "conv_wino_w")) {
-    p.w = c.dwino;
-    HIP_TRY(launch_winow(p, s));
-  } else if (!strcmp(k, "conv_wino_q")) {
+  if (!strcmp(k, "conv_wino_q")) {
     p.w = c.dwino;
     HIP_TRY(launch_winoq(p, s));
   } else if (!strcmp(k, "conv_wino")) {
@@ -418,10 +427,8 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   } else {
     int mt = 2, bn = c.cout_p;  // stem: one N tile (48 fp32 / 64 bf16 channels)
     if (!c.stem) {
-      static const int force_nt = getenv("CLASFV_CONV_NT") ? atoi(getenv("CLASFV_CONV_NT")) : 0;
-      conv_pick_tile(p.M, c.cout_p, force_nt, &mt, &bn);
-      static const int force_mt = getenv("CLASFV_CONV_MT") ? atoi(getenv("CLASFV_CONV_MT")) : 0;
-      if (force_mt == 4 && p.in_bf16) mt = 4;  // A/B switch
+      conv_pick_tile(p.M, c.cout_p, tu.conv_nt, &mt, &bn);
+      if (tu.conv_mt == 4 && p.in_bf16) mt = 4;  // tuning override
     }
     HIP_TRY(launch_conv(p, mt, bn, s));
   }
@@ -505,7 +512,7 @@ struct DeviceGuard {
 extern "C" {
 
 const char* clasfv_last_error(void) { return g_err.c_str(); }
-int clasfv_version(void) { return 1; }
+int clasfv_version(void) { return CLASFV_ABI_VERSION; }
 
 int clasfv_create(int device, clasfv_t* out) {
   if (!out) return fail(CLASFV_EINVAL, "null out");
@@ -514,6 +521,10 @@ int clasfv_create(int device, clasfv_t* out) {
   if (device < 0 || device >= n) return fail(CLASFV_EINVAL, "bad device index");
   auto* e = new clasfv_engine();
   e->device = device;
+  e->tune.vflags = env_variants();
+  e->tune.conv_nt = env_int("CLASFV_CONV_NT");
+  e->tune.conv_mt = env_int("CLASFV_CONV_MT");
+  e->tune.patch_nt = env_int("CLASFV_PATCH_NT");
   build_plan(e);
   *out = e;
   return CLASFV_OK;
@@ -526,7 +537,6 @@ int clasfv_destroy(clasfv_t h) {
     (void)hipFree(c.dw);
     (void)hipFree(c.db);
     (void)hipFree(c.dwino);
-    (void)hipFree(c.dwinor);
     (void)hipFree(c.dwinot);
     (void)hipFree(c.dws16);
   }
@@ -588,12 +598,11 @@ int clasfv_finalize(clasfv_t h) {
     (void)hipFree(c.dw);
     (void)hipFree(c.db);
     (void)hipFree(c.dwino);
-    (void)hipFree(c.dwinor);
     (void)hipFree(c.dwinot);
     (void)hipFree(c.dws16);
     c.dw = c.dws16 = nullptr;
     c.db = nullptr;
-    c.dwino = c.dwinor = c.dwinot = nullptr;
+    c.dwino = c.dwinot = nullptr;
     bn_scale_shift(h, c.bn, c.cout, s, t);
     const auto& w = P(h, c.w + ".weight");
     const int taps = c.kt * c.kh * c.kw;
@@ -601,18 +610,13 @@ int clasfv_finalize(clasfv_t h) {
     int rc = upload_conv(
         c, [&](int o, int ci, int tap) { return w[((size_t)o * cin + ci) * taps + tap]; }, s, t, true);
     if (rc) return rc;
-    if (use_wino(c, bf16)) {
+    if (use_wino(c, bf16, h->tune.vflags)) {
       std::vector<double> wf((size_t)c.cout * cin * 9);
       for (int o = 0; o < c.cout; ++o)
         for (size_t i = 0; i < (size_t)cin * 9; ++i) wf[(size_t)o * cin * 9 + i] = (double)w[(size_t)o * cin * 9 + i] * s[o];
       std::vector<float> u((size_t)16 * c.cin_p * c.cout_p);
       wino_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, u.data());
       if ((rc = upload(u, &c.dwino))) return rc;
-      if (use_winor(c, bf16)) {
-        std::vector<float> ur((size_t)24 * c.cin_p * c.cout_p);
-        winor_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, ur.data());
-        if ((rc = upload(ur, &c.dwinor))) return rc;
-      }
     }
     if (bf16 && c.stem && c.cout_p == 64 && c.kh == 7 && c.kw == 7 && cin <= 4) {  // conv_stem_bf16's K order
       const size_t img = (size_t)64 * 7 * 8 * 4;
@@ -631,7 +635,7 @@ int clasfv_finalize(clasfv_t h) {
             }
       if ((rc = upload_bf16(ws, &c.dws16))) return rc;
     }
-    if (use_winot(c, bf16)) {
+    if (use_winot(c, bf16, h->tune.vflags)) {
       std::vector<double> wf((size_t)c.cout * cin * 3);
       for (int o = 0; o < c.cout; ++o)
         for (size_t i = 0; i < (size_t)cin * 3; ++i) wf[(size_t)o * cin * 3 + i] = (double)w[(size_t)o * cin * 3 + i] * s[o];
@@ -716,6 +720,16 @@ int clasfv_set_compute_dtype(clasfv_t h, int dtype) {
 
 int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; }
 
+int clasfv_set_kernel_variants(clasfv_t h, int flags) {
+  if (!h) return fail(CLASFV_EINVAL, "null handle");
+  if (flags & ~0xFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
+  h->tune.vflags = flags;
+  return CLASFV_OK;
+}
+
+int clasfv_get_kernel_variants(clasfv_t h) { return h ? h->tune.vflags : CLASFV_EINVAL; }
+
 int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float* seg, float* mot, void* stream) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
   if (!h->ready) return fail(CLASFV_ENOTREADY, "clasfv_finalize has not been called");
@@ -747,7 +761,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   auto run = [&](const Conv& c, const void* xin, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
                  const void* x2 = nullptr, int x_c8 = 0, int y_c8 = 0) {
     const char* kname = "";
-    int rc_ = run_conv(c, xin, in, y, out, res, relu, s, h->zero, x2, &kname, x_c8, y_c8);
+    int rc_ = run_conv(c, xin, in, y, out, res, relu, s, h->zero, x2, &kname, h->tune, x_c8, y_c8);
     if (!rc_) timed(kname, conv_gflop(c, out), conv_exec_gflop(c, out, kname));
     return rc_;
   };
@@ -758,7 +772,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   int rc;
   size_t ci = 0;
   // Conv2Plus1D mid tensors (and the stem's) are 8-channel-blocked where c8_pair allows
-  const int c8s = c8_pair(h->convs[0], h->convs[1], sx);
+  const int c8s = c8_pair(h->convs[0], h->convs[1], sx, h->tune);
   if ((rc = run(h->convs[ci++], buf(XIN), sx, buf(S0), s0, nullptr, true, nullptr, 0, c8s))) return rc;
   if ((rc = run(h->convs[ci++], buf(S0), s0, buf(X0), sx0, nullptr, true, nullptr, c8s, 0))) return rc;
   const int outs[4][2] = {{L1A, L1}, {L2A, L2}, {L3A, L3}, {L4A, L4}};
@@ -775,10 +789,10 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
       const Conv& tp2 = h->convs[ci++];
       const Conv* ds = (ci < h->convs.size() && h->convs[ci].role == DS) ? &h->convs[ci++] : nullptr;
       Shape5 sm, sa, sm2, so, sd;
-      const int c8a = c8_pair(sp1, tp1, cs);
+      const int c8a = c8_pair(sp1, tp1, cs, h->tune);
       if ((rc = run(sp1, cur, cs, buf(MID), sm, nullptr, true, nullptr, 0, c8a))) return rc;
       if ((rc = run(tp1, buf(MID), sm, buf(TA), sa, nullptr, true, nullptr, c8a, 0))) return rc;
-      const int c8b = c8_pair(sp2, tp2, sa);
+      const int c8b = c8_pair(sp2, tp2, sa, h->tune);
       if ((rc = run(sp2, buf(TA), sa, buf(MID), sm2, nullptr, true, nullptr, 0, c8b))) return rc;
       const void* res = cur;
       if (ds) {
@@ -821,8 +835,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   d.seg = seg;
   d.mot = mot;
   d.N = N, d.T = T, d.H = H, d.W = W;
-  static const bool no_dec_bf16 = getenv("CLASFV_NO_DECODER_BF16") != nullptr;  // A/B switch (tests)
-  d.bf16 = h->dtype == CLASFV_DTYPE_BF16 && !no_dec_bf16;
+  d.bf16 = h->dtype == CLASFV_DTYPE_BF16 && !(h->tune.vflags & CLASFV_VARIANT_NO_DECODER_BF16);
   HIP_TRY(launch_decoder(d, s));
   // comb_2 (64x64; three split-bf16 products in bf16 engines) and the heads (6 useful of the 16 rows
   // of their MFMA tile) per output voxel
@@ -902,7 +915,8 @@ int clasfv_fuse_votes(const uint8_t* labels, int K, int T, int step, int H, int 
                       void* stream) {
   if (!labels || !fused || K < 1 || K > CLASFV_MAX_PASSES || T < 1 || step < 1 || T - (step - 1) < 1)
     return fail(CLASFV_EINVAL, "bad argument (K must be in [1, 64])");
-  if (method != CLASFV_FUSE_MAJORITY && method != CLASFV_FUSE_SIMPLE && method != CLASFV_FUSE_STAPLE)
+  const int m = method & ~CLASFV_FUSE_FORCE_GENERIC;
+  if (m != CLASFV_FUSE_MAJORITY && m != CLASFV_FUSE_SIMPLE && m != CLASFV_FUSE_STAPLE && m != CLASFV_FUSE_ITKVOTING)
     return fail(CLASFV_EINVAL, "unknown method");
   HIP_TRY(launch_fuse_votes(labels, K, T, step, H * W, method, fused, (hipStream_t)stream));
   return CLASFV_OK;

@@ -17,6 +17,7 @@
 
 #include "common.h"
 
+#include "clasfv.h"
 #include "plumbing.h"
 
 // Every fused multiply-add below is written out (fmaf) where PyTorch's CPU kernels contract one;
@@ -150,8 +151,11 @@ __device__ inline int n_votes(int i, int K, int step) {
   return nv;
 }
 
+// Majority: ties -> background (0). ITK voting (itk::LabelVotingImageFilter with its default
+// undecided label, max input label + 1): ties -> 2 (a tie of two labels needs both present, so the
+// frame's max label is 1). PARITY UNPINNED: LabelFusion / SimpleITK are not available.
 __global__ void fuse_majority_kernel(const uint8_t* __restrict__ labels, int K, int T, int step, int HW,
-                                     uint8_t* __restrict__ fused) {
+                                     uint8_t tie_label, uint8_t* __restrict__ fused) {
   const int o = blockIdx.y;
   const int i = o == 0 ? 0 : o + step - 1;
   const int nv = o == 0 ? 1 : n_votes(i, K, step);
@@ -159,7 +163,7 @@ __global__ void fuse_majority_kernel(const uint8_t* __restrict__ labels, int K, 
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
     int ones = 0;
     for (int idx = 0; idx < nv; ++idx) ones += labels[((size_t)idx * T + (i - idx * step)) * HW + p];
-    out[p] = (nv == 1) ? (uint8_t)ones : (uint8_t)(2 * ones > nv ? 1 : 0);
+    out[p] = (nv == 1) ? (uint8_t)ones : 2 * ones == nv ? tie_label : (uint8_t)(2 * ones > nv ? 1 : 0);
   }
 }
 
@@ -740,11 +744,13 @@ hipError_t launch_logit_margin(const float* logits, int n, int HW, float* margin
 hipError_t launch_fuse_votes(const uint8_t* labels, int K, int T, int step, int HW, int method, uint8_t* fused,
                              hipStream_t s) {
   const int tout = T - (step - 1);
+  const bool force_generic = (method & CLASFV_FUSE_FORCE_GENERIC) != 0;  // A/B testing of the SIMPLE kernels
+  method &= ~CLASFV_FUSE_FORCE_GENERIC;
   if (method == 2) {
     hipLaunchKernelGGL(fuse_staple_kernel, dim3(tout), dim3(STAPLE_THREADS), 0, s, labels, K, T, step, HW, fused);
   } else if (method == 1) {
     const size_t lds = 3 * (size_t)HW;
-    if (K <= SIMPLE_FAST_MAXV && lds <= 160 * 1024 && !getenv("CLASFV_SIMPLE_GENERIC")) {
+    if (K <= SIMPLE_FAST_MAXV && lds <= 160 * 1024 && !force_generic) {
       static size_t attr = 0;
       if (lds > 64 * 1024 && lds > attr) {
         hipError_t e = hipFuncSetAttribute((const void*)fuse_simple_fast_kernel,
@@ -759,7 +765,8 @@ hipError_t launch_fuse_votes(const uint8_t* labels, int K, int T, int step, int 
     }
   } else {
     dim3 grid(blocks_for(HW, 256, 64), tout);
-    hipLaunchKernelGGL(fuse_majority_kernel, grid, dim3(256), 0, s, labels, K, T, step, HW, fused);
+    const uint8_t tie = method == 3 ? 2 : 0;  // CLASFV_FUSE_ITKVOTING
+    hipLaunchKernelGGL(fuse_majority_kernel, grid, dim3(256), 0, s, labels, K, T, step, HW, tie, fused);
   }
   return hipGetLastError();
 }

@@ -501,16 +501,16 @@ bool winot5_fits(const ConvParams& p) { return (size_t)p.N * p.Ti * p.Hi * p.Wi 
 }  // namespace
 
 bool winot_c8_ok(const ConvParams& p) {
-  return winot_supported(p) && getenv("CLASFV_WINOT_REFERENCE") == nullptr && p.Ti % 8 == 0 && winot5_fits(p);
+  return winot_supported(p) && !(p.vflags & CLASFV_VARIANT_WINOT_REFERENCE) && p.Ti % 8 == 0 && winot5_fits(p);
 }
 
 // conv_winot5 for channels-last input: T % 8 == 0 in time-adjacent tile pairs, other T % 4 == 0 (one
-// tile row per segment) in column-adjacent pairs (TS = 1); CLASFV_WINOT_TS1=0 keeps the latter on
-// conv_winot
+// tile row per segment) in column-adjacent pairs (TS = 1); CLASFV_VARIANT_WINOT_NO_TS1 keeps the
+// latter on conv_winot
 static bool winot5_ok(const ConvParams& p) {
   if (winot_c8_ok(p)) return true;
-  static const bool ts1 = [] { const char* e = getenv("CLASFV_WINOT_TS1"); return !(e && e[0] == '0'); }();
-  return ts1 && !p.x_c8 && winot_supported(p) && getenv("CLASFV_WINOT_REFERENCE") == nullptr && winot5_fits(p);
+  return !(p.vflags & (CLASFV_VARIANT_WINOT_NO_TS1 | CLASFV_VARIANT_WINOT_REFERENCE)) && !p.x_c8 && winot_supported(p) &&
+         winot5_fits(p);
 }
 
 bool winot_supported(const ConvParams& p) {
@@ -523,7 +523,7 @@ bool winot_supported(const ConvParams& p) {
 // U: [Cin/8][6][Cout/64][64][8] transformed weights (winot_transform_weights).
 hipError_t launch_winot(const ConvParams& p, hipStream_t s) {
   if (!winot_supported(p)) return hipErrorInvalidValue;
-  // CLASFV_WINOT_REFERENCE=1 (tests): always conv_winot; both kernels compute the same products in
+  // CLASFV_VARIANT_WINOT_REFERENCE (tests): always conv_winot; both kernels compute the same products in
   // the same order (bit-identical outputs).
   if (winot5_ok(p)) return winot5_dispatch(p, s);
   if (p.x_c8) return hipErrorInvalidValue;  // 8-channel-blocked input: conv_winot5 only

@@ -136,21 +136,46 @@ def exchange_to_owners(local, owners, rank, world, group=None):
     return out  # source blocks are in rank order and each is in global order: global order overall
 
 
+def videos_needed(lengths, num_clips, step, rank, world, interpolate_last=True):
+    """Indices of the videos rank must hold on its device: those with a clip in its block. A rank
+    only materialises these (e.g. config[2], 64 videos over 8 ranks: 8 per rank)."""
+    plans, n_total = global_clip_plan(lengths, num_clips, step, interpolate_last)
+    lo, hi = shard_bounds(n_total, rank, world)
+    return [vi for vi, p in enumerate(plans) if max(lo, p["offset"]) < min(hi, p["offset"] + p["n"])]
+
+
+def exchange_stats(lengths, num_clips, step, world, h=112, w=112, interpolate_last=True):
+    """(clips crossing ranks, bytes on the wire) of one sharded pass over videos of these lengths:
+    one fp32 logit-margin plane of 32 frames per exchanged clip."""
+    plans, _ = global_clip_plan(lengths, num_clips, step, interpolate_last)
+    rows = rows_exchanged(owner_of_clips(plans, world), world) if world > 1 else 0
+    return rows, rows * FU.CLIP * h * w * 4
+
+
 def segment_videos_sharded(videos_dev, model, num_clips=5, step=1, fuse_method="simple", interpolate_last=True,
-                           rank=0, world=1, batch_size=None, clip_fn=None):
+                           rank=0, world=1, batch_size=None, clip_fn=None, lengths=None):
     """Fuse a batch of device videos (each (3,T,H,W)) with clips sharded over ranks.
 
     Returns {video index: fused (T',H,W) uint8 device tensor} for the videos this rank owns
-    (video_owners). ``clip_fn(clips) -> logits`` overrides the model call."""
-    plans, n_total = global_clip_plan([v.shape[1] for v in videos_dev], num_clips, step, interpolate_last)
-    h, w = videos_dev[0].shape[-2:]
-    dev = videos_dev[0].device
+    (video_owners). ``clip_fn(clips) -> logits`` overrides the model call. With ``lengths`` (the
+    frame count of every video) ``videos_dev`` may hold None for videos outside this rank's block
+    (``videos_needed``)."""
+    if lengths is None:
+        lengths = [v.shape[1] for v in videos_dev]
+    plans, n_total = global_clip_plan(list(lengths), num_clips, step, interpolate_last)
+    present = [v for v in videos_dev if v is not None]
+    if not present:
+        raise ValueError("no video tensor on this rank")
+    h, w = present[0].shape[-2:]
+    dev = present[0].device
 
     def compute(lo, hi):
         mine = []
         for vi, p in enumerate(plans):  # overlap of each video's clip range with [lo, hi)
             a, b = max(lo, p["offset"]), min(hi, p["offset"] + p["n"])
             if a < b:
+                if videos_dev[vi] is None:
+                    raise ValueError(f"video {vi} has clips in rank {rank}'s block but is not on this rank")
                 mine.append(FU.build_clips(videos_dev[vi], p["table"][a - p["offset"]: b - p["offset"]],
                                            interpolate_last))
         clips = torch.cat(mine) if len(mine) > 1 else mine[0]

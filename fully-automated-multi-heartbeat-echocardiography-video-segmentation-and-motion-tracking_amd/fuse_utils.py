@@ -8,11 +8,17 @@ reference, but every clip of every temporally shifted pass is built on the GPU
 stay in HBM (``clasfv_pass_labels``, ``clasfv_fuse_votes``); only the final uint8 mask crosses PCIe.
 
 Reference behaviour kept: banker's rounding of the clip count (:22,29), the K clamp and its
-"Video is too short" message (:38-42), IndexError when K == 0 (:82, e.g. T == 32), frames 1..step-1
-dropped for step > 1 (:85), passes with different clip counts (numpy 1.19 ragged arrays, :50).
-Fusion: ``majority`` (= ``majorityvoting``/``mv``/``itkvoting``; ties -> background), ``simple``
-(SIMPLE, Langerak 2010) and ``staple`` (STAPLE, Warfield 2004), up to 64 passes. LabelFusion itself
-is not available, so ``simple`` and ``staple`` are parity-unpinned.
+"Video is too short" message (:38-42), passes with different clip counts (numpy 1.19 ragged arrays,
+:50). Two reference quirks are reproduced by default (``strict_reference=True``) and corrected with
+``strict_reference=False``: K == 0 after the clamp (T in [32, 32 + step), e.g. a single 32-frame
+clip) raises IndexError at :82 -- non-strict runs the one unshifted pass; frames 1..step-1 are
+dropped for step > 1 (:85) -- non-strict keeps them with their single (pass 0) vote, so the output
+always has T frames.
+Fusion: ``majority`` (= ``majorityvoting``/``mv``; ties -> background), ``itkvoting`` (= ``voting``;
+itk::LabelVotingImageFilter with its default undecided label: ties -> 2), ``simple`` (SIMPLE,
+Langerak 2010) and ``staple`` (STAPLE, Warfield 2004), up to 64 passes. LabelFusion itself is not
+available, so every rule but ``majority`` (pinned by the reference-run goldens of its stub) is
+parity-unpinned.
 """
 import numpy as np
 import torch
@@ -20,7 +26,7 @@ import torch
 from . import _lib
 
 FUSE_METHODS = {"majority": _lib.FUSE_MAJORITY, "majorityvoting": _lib.FUSE_MAJORITY, "mv": _lib.FUSE_MAJORITY,
-                "itkvoting": _lib.FUSE_MAJORITY, "voting": _lib.FUSE_MAJORITY, "simple": _lib.FUSE_SIMPLE,
+                "itkvoting": _lib.FUSE_ITKVOTING, "voting": _lib.FUSE_ITKVOTING, "simple": _lib.FUSE_SIMPLE,
                 "staple": _lib.FUSE_STAPLE}
 MAX_PASSES = 64  # CLASFV_MAX_PASSES
 CLIP = 32
@@ -32,14 +38,31 @@ def n_clips(t, clip_length=CLIP):
     return int(np.round(t / clip_length))
 
 
-def clamp_num_clips(t, num_clips, step):
-    """src/fuse_utils.py:38-42."""
+def clamp_num_clips(t, num_clips, step, strict_reference=True):
+    """src/fuse_utils.py:38-42. The reference can clamp to K == 0 (T in [32, 32 + step)), which then
+    fails at :82; with strict_reference=False that case runs the one unshifted pass instead."""
     if t < CLIP + num_clips * step:
         num_clips = (t - CLIP) // step
     if num_clips < 0:
         print("Video is too short")
         num_clips = 1
+    if num_clips == 0 and not strict_reference:
+        num_clips = 1
     return num_clips
+
+
+def fused_frames(t, step, strict_reference=True):
+    """Frames of the fused output: the reference drops frames 1..step-1 (src/fuse_utils.py:85)."""
+    return t if not strict_reference else t - (step - 1)
+
+
+def keep_dropped_frames(labels, fused, step):
+    """Non-strict output: the strict fused video (frames 0, step, step+1, ...) with frames 1..step-1
+    re-inserted. Those frames have a single vote -- pass 0's label, as the reference's own loop would
+    give them if it did not skip them (:85-93)."""
+    if step == 1:
+        return fused
+    return torch.cat([fused[:1], labels[0, 1:step].to(fused.dtype), fused[1:]])
 
 
 def clip_table(t, num_passes, step, interpolate_last=True):
@@ -123,12 +146,16 @@ def run_model(model, clips, batch_size=None):
     return torch.cat(outs) if len(outs) > 1 else outs[0].contiguous()
 
 
-def fuse_votes(labels, step, fuse_method="simple"):
+def fuse_votes(labels, step, fuse_method="simple", force_generic=False):
+    """Per-frame fusion of (K,T,H,W) uint8 pass labels -> (T-(step-1),H,W) uint8. ``force_generic``
+    runs SIMPLE on its generic kernel instead of the packed <= 16-vote one (A/B tests)."""
     labels = labels.to(torch.uint8).contiguous()
     k, t, h, w = labels.shape
     method = FUSE_METHODS.get(fuse_method.lower())
     if method is None:
         raise NotImplementedError(f"fuse_method {fuse_method!r}: supported {sorted(FUSE_METHODS)}")
+    if force_generic:
+        method |= _lib.FUSE_FORCE_GENERIC
     fused = torch.empty((t - (step - 1), h, w), device=labels.device, dtype=torch.uint8)
     lib = _lib.load()
     _lib.check(lib.clasfv_fuse_votes(_lib.ptr(labels), k, t, step, h, w, method, _lib.ptr(fused),
@@ -144,21 +171,22 @@ def ctypes_int32_array(vals):
 
 
 def segment_a_video_with_fusion_device(video, model, interpolate_last=True, step=1, num_clips=10, fuse_method="simple",
-                                       class_list=(0, 1), batch_size=None):
+                                       class_list=(0, 1), batch_size=None, strict_reference=True):
     """Same as segment_a_video_with_fusion but returns the fused (T',H,W) uint8 mask on the device."""
     if list(class_list) != [0, 1]:
         raise ValueError("the engine fuses the two CLAS-FV classes [0, 1]")
     dev = _device_of(model)
     v = to_device_video(video, dev)
     t = v.shape[1]
-    k = clamp_num_clips(t, num_clips, step)
+    k = clamp_num_clips(t, num_clips, step, strict_reference)
     if k == 0:
         raise IndexError("list index out of range")  # src/fuse_utils.py:82 with no pass
     table, clip0 = clip_table(t, k, step, interpolate_last)
     clips = build_clips(v, table, interpolate_last)
     logits = run_model(model, clips, batch_size)
     labels = pass_labels(logits, clip0, t, step, interpolate_last)
-    return fuse_votes(labels, step, fuse_method)
+    fused = fuse_votes(labels, step, fuse_method)
+    return fused if strict_reference else keep_dropped_frames(labels, fused, step)
 
 
 def logit_margin(logits):
@@ -191,8 +219,9 @@ def pass_labels(logits, clip0, t, step, interpolate_last=True, margin=False):
 
 
 def segment_a_video_with_fusion(video, model, interpolate_last=True, step=1, num_clips=10, fuse_method="simple",
-                                class_list=[0, 1], batch_size=None):
-    """src/fuse_utils.py:36-100 -> numpy int64 (T', H, W)."""
+                                class_list=[0, 1], batch_size=None, strict_reference=True):
+    """src/fuse_utils.py:36-100 -> numpy int64 (T', H, W). ``strict_reference=False`` corrects the
+    two reference quirks (see the module docstring): T' == T always, and T == 32 yields masks."""
     fused = segment_a_video_with_fusion_device(video, model, interpolate_last, step, num_clips, fuse_method, class_list,
-                                               batch_size)
+                                               batch_size, strict_reference)
     return fused.to(torch.int64).cpu().numpy()

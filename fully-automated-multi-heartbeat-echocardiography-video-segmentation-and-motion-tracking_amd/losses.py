@@ -97,9 +97,12 @@ def _propagate(seeds, fields, direction, start, end):
     """Advance label chains through per-frame displacement fields.
 
     seeds: {name: (first_frame, one-hot (N,2,H,W))}; a chain seeded at frame f is warped by
-    fields[:, :, f] and lands on f + direction, then by the field of that frame, and so on while the
-    landing frame stays inside [start, end). Chains active at the same frame are stacked into one
-    warp launch. Returns {name: [(landing_frame, warped label), ...]} in propagation order."""
+    fields[:, :, f] and lands on f + direction, then by the field of that frame, and so on. As in the
+    reference's loops, forward chains run while the landing frame is < end (range(seed, end - 1),
+    src/clasfv_losses.py:83,97) and backward chains while the warped frame is > start
+    (range(seed, start, -1), :111,125): neither direction looks at the other bound. Chains active
+    at the same frame are stacked into one warp launch. Returns {name: [(landing_frame, warped
+    label), ...]} in propagation order."""
     n = fields.shape[0]
     frames = {k: f for k, (f, _) in seeds.items()}
     state = {k: lab for k, (_, lab) in seeds.items()}
@@ -108,7 +111,7 @@ def _propagate(seeds, fields, direction, start, end):
     f = first
     while True:
         land = f + direction
-        if not (start <= land < end) or (direction < 0 and f <= start):
+        if (land >= end) if direction > 0 else (f <= start):
             break
         active = [k for k in seeds if (frames[k] <= f if direction > 0 else frames[k] >= f)]
         if active:

@@ -6,8 +6,10 @@ the reference's 242 keys; ``load_state_dict`` accepts the ``module.``-prefixed k
 ``nn.DataParallel`` checkpoints carry (motion_segment.py:69-72).
 
 Differences, all deliberate:
-* ``pretrained=True`` cannot download Kinetics weights offline; the network starts from the seeded
-  synthetic weights (weights.synthetic_state_dict) and a checkpoint is expected to be loaded.
+* ``pretrained=True`` cannot download Kinetics weights offline; the network starts from seeded
+  synthetic weights (``weights="random"``: weights.synthetic_state_dict; ``weights="echo"``: the
+  recipe whose masks follow the synthetic video's LV, weights.echo_state_dict) and a checkpoint is
+  expected to be loaded.
 * Inference only: forward runs under no autograd (the reference builds graphs it never uses,
   src/fuse_utils.py:59).
 * Any H, W multiple of 16 and T multiple of 8 is accepted (the reference's concat needs the same).
@@ -22,7 +24,7 @@ from torch import nn
 
 from . import _lib
 from .arch import strip_module_prefix
-from .weights import DEFAULT_SEED, synthetic_state_dict
+from .weights import DEFAULT_SEED, recipe_state_dict
 
 
 class Engine:
@@ -45,6 +47,18 @@ class Engine:
             raise ValueError(f"dtype must be one of {sorted(_lib.DTYPES)}")
         _lib.check(self.lib.clasfv_set_compute_dtype(self.h, _lib.DTYPES[dtype]), "clasfv_set_compute_dtype")
         self.dtype = "bf16" if _lib.DTYPES[dtype] == 1 else "fp32"
+
+    def set_variants(self, *names):
+        """Kernel variants for A/B tests (CLASFV_VARIANT_*; e.g. "no_winograd"); no names = the
+        product kernels. Returns the previous names. Call load() afterwards if no_winograd changed."""
+        flags = 0
+        for n in names:
+            if n not in _lib.VARIANTS:
+                raise ValueError(f"unknown kernel variant {n!r}: {sorted(_lib.VARIANTS)}")
+            flags |= _lib.VARIANTS[n]
+        old = self.lib.clasfv_get_kernel_variants(self.h)
+        _lib.check(self.lib.clasfv_set_kernel_variants(self.h, flags), "clasfv_set_kernel_variants")
+        return tuple(n for n, b in _lib.VARIANTS.items() if old & b)
 
     def __del__(self):
         try:
@@ -101,7 +115,8 @@ class Engine:
 class R2plus1D_18_MotionNet(nn.Module):
     """HIP-backed drop-in for the reference model (inference)."""
 
-    def __init__(self, pretrained=True, output_channels=4, device=None, seed=DEFAULT_SEED, dtype="fp32"):
+    def __init__(self, pretrained=True, output_channels=4, device=None, seed=DEFAULT_SEED, dtype="fp32",
+                 weights="random"):
         super().__init__()
         if output_channels != 4:
             raise ValueError("the motion head has 4 channels [fwd x, fwd y, bwd x, bwd y]")
@@ -111,7 +126,14 @@ class R2plus1D_18_MotionNet(nn.Module):
         self.engine = Engine(device, dtype)
         self._state = OrderedDict()
         self._params = None
-        self._load(synthetic_state_dict(seed))
+        self._load(recipe_state_dict(weights, seed))
+
+    def set_kernel_variants(self, *names):
+        """A/B-test kernel variants (see Engine.set_variants); weights are re-uploaded so the
+        choice of Winograd or direct weight images follows. Returns the previous variant names."""
+        old = self.engine.set_variants(*names)
+        self.engine.load(self._state)
+        return old
 
     def set_compute_dtype(self, dtype):
         """Switch the encoder between exact fp32 and bf16 (fp32 accumulation) and re-upload weights."""

@@ -5,14 +5,14 @@ conversion, resize and normalisation on the host (:96-106), then batch-1 clip fo
 device->host copy after each (src/fuse_utils.py:53-61) and fusion on the host. Here a stream of
 videos flows through the engine with no host synchronisation between videos:
 
-* each video's uint8 frames (the decoder's output, a quarter of the float video's bytes) are copied
-  from pinned host memory to HBM on a dedicated copy stream, one video ahead of the compute stream,
-  so PCIe overlaps the previous video's forward;
+* each video's uint8 frames (the decoder's output, a quarter of the float video's bytes) are staged
+  in a reused ring of pinned host buffers and copied to HBM on a dedicated copy stream, one video
+  ahead of the compute stream, so PCIe overlaps the previous video's forward;
 * resize + zero-one normalisation (clasfv_preprocess_video / clasfv_zeroone_normalize), clip
   building, the batched forward, softmax -> resample -> argmax and label fusion run on the compute
   stream (fuse_utils.segment_a_video_with_fusion_device);
-* the fused uint8 masks go back to pinned host buffers asynchronously; the host waits once, at the
-  end, and widens them to the reference's int64.
+* the fused uint8 masks go back to one pinned host buffer asynchronously; the host waits once, at
+  the end, and widens them to the reference's int64.
 
 Results are identical to calling segment_a_video_with_fusion per video (same kernels, same inputs).
 """
@@ -24,60 +24,99 @@ from .preprocess import preprocess_video
 
 
 class VideoStream:
-    """``run(frame_videos) -> [int64 (T', H, W) masks]`` for a list of (T, Hs, Ws, 3) uint8 videos."""
+    """``run(frame_videos) -> [int64 (T', H, W) masks]`` for a list of (T, Hs, Ws, 3) uint8 videos.
+
+    All compute is ordered on the stream that is current for the device when ``run`` is called
+    (so ``with torch.cuda.stream(s): vs.run(...)`` works); uploads use a private copy stream and a
+    ring of two pinned staging buffers that is reused across videos and calls."""
+
+    RING = 2
 
     def __init__(self, model, num_clips=5, step=1, fuse_method="simple", height=112, width=112,
-                 batch_size=None, interpolate_last=True):
+                 batch_size=None, interpolate_last=True, strict_reference=True):
         self.model = model
         self.device = FU._device_of(model)
         self.kw = dict(interpolate_last=interpolate_last, step=step, num_clips=num_clips, fuse_method=fuse_method,
-                       batch_size=batch_size)
+                       batch_size=batch_size, strict_reference=strict_reference)
         self.height, self.width = height, width
         self.copy_stream = torch.cuda.Stream(self.device)
-        self.compute_stream = torch.cuda.current_stream(self.device)
+        self._ring = [None] * self.RING     # pinned uint8 staging buffers
+        self._ring_ev = [None] * self.RING  # copy-stream event of the H2D last issued from each slot
+        self._slot = 0
+
+    def _staging(self, nbytes):
+        """Next ring slot with room for nbytes; waits (host) until the H2D last issued from it has
+        finished reading it."""
+        i = self._slot
+        self._slot = (i + 1) % self.RING
+        if self._ring_ev[i] is not None:
+            self._ring_ev[i].synchronize()
+        if self._ring[i] is None or self._ring[i].numel() < nbytes:
+            self._ring[i] = torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=True)
+        return i, self._ring[i][:nbytes]
 
     def _upload(self, frames):
-        """Pinned host copy + async H2D on the copy stream; returns (device tensor, ready event)."""
+        """Copy into a pinned ring slot + async H2D on the copy stream; returns (device tensor, ready event)."""
         host = frames if torch.is_tensor(frames) else torch.from_numpy(np.ascontiguousarray(frames))
         if host.dtype != torch.uint8 or host.dim() != 4 or host.shape[-1] != 3:
             raise ValueError(f"expected (T,H,W,3) uint8 frames, got {tuple(host.shape)} {host.dtype}")
-        if not host.is_pinned():
-            host = host.pin_memory()
+        if host.is_pinned():
+            src, slot = host, None
+        else:
+            slot, buf = self._staging(host.numel())
+            src = buf.view(host.shape)
+            src.copy_(host)
         with torch.cuda.stream(self.copy_stream):
-            dev = host.to(self.device, non_blocking=True)
+            dev = src.to(self.device, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.copy_stream)
-        return dev, ev, host
+        if slot is not None:
+            self._ring_ev[slot] = ev
+        return dev, ev, (host if slot is None else None)
 
     def run(self, frame_videos, return_device=False):
         videos = list(frame_videos)
         if not videos:
             return []
-        outs, keep = [], []
+        compute = torch.cuda.current_stream(self.device)
+        outs, keep, host_out = [], [], []
         pending = self._upload(videos[0])
         for i in range(len(videos)):
-            dev, ev, host = pending
+            dev, ev, pinned_src = pending
             if i + 1 < len(videos):  # the next video's PCIe copy overlaps this video's compute
                 pending = self._upload(videos[i + 1])
-            self.compute_stream.wait_event(ev)
-            dev.record_stream(self.compute_stream)  # allocated on the copy stream, used here
+            compute.wait_event(ev)
+            dev.record_stream(compute)  # allocated on the copy stream, used on the compute stream
             video = preprocess_video(dev, self.height, self.width, device=self.device)
             fused = FU.segment_a_video_with_fusion_device(video, self.model, **self.kw)
             if return_device:
                 outs.append(fused)
             else:
-                h = torch.empty(fused.shape, dtype=torch.uint8, pin_memory=True)
-                h.copy_(fused, non_blocking=True)
-                outs.append(h)
-            keep.append(host)  # pinned source buffers stay alive until the copies retire
-        torch.cuda.current_stream(self.device).synchronize()
-        self.copy_stream.synchronize()
+                outs.append(fused)
+                host_out.append(fused.shape)
+            if pinned_src is not None:
+                keep.append(pinned_src)  # caller-pinned sources stay alive until their copies retire
         if return_device:
+            compute.synchronize()
+            self.copy_stream.synchronize()
             return outs
-        return [o.numpy().astype(np.int64) for o in outs]
+        # one pinned buffer for every mask of the call, filled by async D2H copies on the compute stream
+        total = sum(int(np.prod(sh)) for sh in host_out)
+        flat = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=True)
+        res, at = [], 0
+        for fused in outs:
+            n = fused.numel()
+            dst = flat[at:at + n].view(fused.shape)
+            dst.copy_(fused, non_blocking=True)
+            res.append(dst)
+            at += n
+        compute.synchronize()
+        self.copy_stream.synchronize()
+        return [r.numpy().astype(np.int64) for r in res]
 
 
 def segment_videos(frame_videos, model, num_clips=5, step=1, fuse_method="simple", height=112, width=112,
-                   batch_size=None):
+                   batch_size=None, strict_reference=True):
     """Convenience wrapper: VideoStream(...).run(frame_videos)."""
-    return VideoStream(model, num_clips, step, fuse_method, height, width, batch_size).run(frame_videos)
+    return VideoStream(model, num_clips, step, fuse_method, height, width, batch_size,
+                       strict_reference=strict_reference).run(frame_videos)

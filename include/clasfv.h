@@ -40,12 +40,39 @@ enum {
   CLASFV_ENOMEM = -5
 };
 
-enum { CLASFV_FUSE_MAJORITY = 0, CLASFV_FUSE_SIMPLE = 1, CLASFV_FUSE_STAPLE = 2 };
+/* ABI revision: bumped whenever an exported function changes its parameter list. Callers check
+ * clasfv_version() == CLASFV_ABI_VERSION after loading the library (the ctypes binding does).
+ *   1  round 1
+ *   2  clasfv_zeroone_normalize takes a caller-owned workspace; clasfv_kernel_timing reports xgflop
+ *   3  kernel variants (clasfv_set_kernel_variants), CLASFV_FUSE_FORCE_GENERIC */
+#define CLASFV_ABI_VERSION 3
+
+/* MAJORITY: ties -> 0; ITKVOTING: itk::LabelVotingImageFilter with its default undecided label
+ * (max label + 1): ties -> 2. */
+enum { CLASFV_FUSE_MAJORITY = 0, CLASFV_FUSE_SIMPLE = 1, CLASFV_FUSE_STAPLE = 2, CLASFV_FUSE_ITKVOTING = 3 };
+/* OR-ed into a clasfv_fuse_votes method: run SIMPLE on its generic kernel instead of the packed
+ * 16-vote one (A/B testing; results are identical). */
+#define CLASFV_FUSE_FORCE_GENERIC 0x100
 enum { CLASFV_DTYPE_FP32 = 0, CLASFV_DTYPE_BF16 = 1 };
+
+/* Kernel-variant switches (A/B testing against the kernels each product kernel replaced; every
+ * variant computes the same function). Read once, at clasfv_create, from the environment variable
+ * named in the comment (set = on), or set with clasfv_set_kernel_variants. */
+enum {
+  CLASFV_VARIANT_NO_WINOGRAD = 1,      /* CLASFV_WINOGRAD=0: fp32 stride-1 convs on the direct implicit GEMM */
+  CLASFV_VARIANT_NO_WINO_PATCH = 2,    /* CLASFV_NO_WINO_PATCH: conv_wino instead of conv_wino_q */
+  CLASFV_VARIANT_WINOT_REFERENCE = 4,  /* CLASFV_WINOT_REFERENCE: conv_winot instead of conv_winot5 */
+  CLASFV_VARIANT_NO_C8 = 8,            /* CLASFV_NO_C8: channels-last mid tensors everywhere */
+  CLASFV_VARIANT_NO_STEM_BF16 = 16,    /* CLASFV_NO_STEM_BF16: bf16 engines run the fp32 stem */
+  CLASFV_VARIANT_NO_PATCH_BF16 = 32,   /* CLASFV_NO_PATCH_BF16: bf16 stride-1 convs on conv_dma */
+  CLASFV_VARIANT_NO_DECODER_BF16 = 64, /* CLASFV_NO_DECODER_BF16: bf16 engines run the fp32 decoder */
+  CLASFV_VARIANT_WINOT_NO_TS1 = 128    /* CLASFV_WINOT_TS1=0: T % 8 != 0 temporal convs on conv_winot */
+};
 
 typedef struct clasfv_engine* clasfv_t;
 
 const char* clasfv_last_error(void);
+/* CLASFV_ABI_VERSION of the loaded library. */
 int clasfv_version(void);
 
 /* ---- model: replaces R2plus1D_18_MotionNet.__init__/load_state_dict/forward ------------------ */
@@ -71,6 +98,11 @@ int64_t clasfv_workspace_bytes(clasfv_t h);
  * clasfv_finalize. */
 int clasfv_set_compute_dtype(clasfv_t h, int dtype);
 int clasfv_get_compute_dtype(clasfv_t h);
+/* Kernel-variant switches (CLASFV_VARIANT_* bits). A change of CLASFV_VARIANT_NO_WINOGRAD needs the
+ * next clasfv_finalize (the Winograd weight images are built there); the others apply to the next
+ * clasfv_forward. */
+int clasfv_set_kernel_variants(clasfv_t h, int flags);
+int clasfv_get_kernel_variants(clasfv_t h);
 
 /* ---- instrumentation (bench.py's live roofline; not on the reference's interface) ------------ */
 /* enable != 0: every later clasfv_forward records one HIP event on its stream before its first
@@ -107,9 +139,10 @@ int clasfv_pass_labels_margin(const float* margin_dev, int K, const int32_t* pas
 /* margin_dev (n,32,H,W) = logits_dev[:,1] - logits_dev[:,0] for n clips of (2,32,H,W) logits. */
 int clasfv_logit_margin(const float* logits_dev, int n, int H, int W, float* margin_dev, void* stream);
 /* Per-frame label fusion over the K <= 64 shifted passes (fuse_utils.py:82-100). Output (T',H,W)
- * uint8 with T' = T - (step - 1). method: CLASFV_FUSE_MAJORITY, CLASFV_FUSE_SIMPLE or
- * CLASFV_FUSE_STAPLE (LabelFusion's methods, fuse_utils.py:95; SIMPLE and STAPLE are restated from
- * their papers: LabelFusion itself is absent, so their parity is unpinned). */
+ * uint8 with T' = T - (step - 1). method: CLASFV_FUSE_MAJORITY, CLASFV_FUSE_SIMPLE,
+ * CLASFV_FUSE_STAPLE or CLASFV_FUSE_ITKVOTING (LabelFusion's methods, fuse_utils.py:95; SIMPLE,
+ * STAPLE and ITK voting are restated from their published definitions: LabelFusion itself is absent,
+ * so their parity is unpinned). */
 int clasfv_fuse_votes(const uint8_t* labels_dev, int K, int T, int step, int H, int W, int method,
                       uint8_t* fused_dev, void* stream);
 

@@ -1,13 +1,14 @@
 """Drop-in for the reference CLI ``motion_segment.py`` (flags :19-65, outputs :117-150) on the
 MI355X engine: segment and motion-track the LV in an echo video, print EF, write pickles.
 
-Same flags and defaults. ``-d/--device`` keeps the reference default ``cpu``: there, as in the
-reference (whose ``nn.DataParallel`` scatters host tensors to GPU 0 whenever a GPU is visible,
-motion_segment.py:69-70), the video and the outputs live on the host and the engine runs on GPU 0 --
-a notice says so. There is no CPU compute path: without a GPU the CLI exits with an error.
-``-d cuda`` / ``cuda:i`` keep the video on that GPU end to end.
-Extra opt-in flags: ``--synthetic-weights SEED`` (seeded random weights when no checkpoint is
-available offline) and ``--batch-size`` (clips per forward call).
+Same flags and defaults. ``-d/--device`` keeps the reference default ``cpu``. In the reference that
+runs the model on the host CPU; this engine has no CPU compute path, so -- a deliberate extension,
+announced by a notice -- ``-d cpu`` runs the engine on GPU 0 and returns host arrays, exactly as
+``-d cuda`` does (the outputs are numpy int64 arrays either way). Without a GPU the CLI exits with
+an error. ``-d cuda`` / ``cuda:i`` pick the GPU.
+Extra opt-in flags: ``--synthetic-weights SEED`` with ``--synthetic-recipe echo|random`` (seeded
+weights when no checkpoint is available offline), ``--batch-size`` (clips per forward call) and
+``--no-strict-reference`` (fuse_utils.segment_a_video_with_fusion(strict_reference=False)).
 Video input: any file OpenCV can decode if cv2 is installed (as the reference), or ``.npy`` holding
 (T,H,W,3) uint8 RGB frames.
 """
@@ -40,7 +41,13 @@ def parse_args(argv=None):
     ap.add_argument("--width", required=False, type=int, help="Width of image (pretrain model uses 112)", default=112)
     ap.add_argument("--synthetic-weights", type=int, default=None, metavar="SEED",
                     help="use seeded synthetic weights instead of a checkpoint (no trained weights offline)")
+    ap.add_argument("--synthetic-recipe", choices=["echo", "random"], default="echo",
+                    help="synthetic weight recipe: 'echo' segments the LV of EchoNet-style videos (physiological "
+                         "EFs), 'random' is plain seeded noise")
     ap.add_argument("--batch-size", type=int, default=32, help="clips per forward call")
+    ap.add_argument("--no-strict-reference", action="store_true",
+                    help="correct the reference's plumbing quirks: a single 32-frame clip yields masks instead of "
+                         "IndexError, and frames 1..step-1 are kept for step > 1")
     return ap.parse_args(argv)
 
 
@@ -73,8 +80,8 @@ def main(argv=None):
     if not torch.cuda.is_available():
         sys.exit("error: the CLAS-FV engine needs an MI355X (ROCm) GPU and none is visible")
     if host_io:
-        print("notice: -d cpu: video and outputs stay in host memory; the engine runs on GPU 0 "
-              "(as the reference's DataParallel scatters host tensors to GPU 0)", file=sys.stderr)
+        print("notice: -d cpu: this engine has no CPU compute path; the engine runs on GPU 0 and the outputs "
+              "are host arrays", file=sys.stderr)
         dev = torch.device("cuda", 0)
     else:
         dev = torch.device(args.device)
@@ -91,7 +98,7 @@ def main(argv=None):
     from clasfv_amd.weights import DEFAULT_SEED, load_checkpoint
 
     seed = args.synthetic_weights if args.synthetic_weights is not None else DEFAULT_SEED
-    model = R2plus1D_18_MotionNet(pretrained=False, seed=seed, device=dev)
+    model = R2plus1D_18_MotionNet(pretrained=False, seed=seed, device=dev, weights=args.synthetic_recipe)
     if args.synthetic_weights is None:
         model.load_state_dict(load_checkpoint(args.model))
     if args.verbose:
@@ -100,12 +107,11 @@ def main(argv=None):
 
     # motion_segment.py:96-106 on the device: uint8 frames -> resize -> zero-one normalisation
     video = preprocess_video(read_video(args.path), args.height, args.width, device=dev)
-    if host_io:  # the reference's -d cpu video is a host array handed to the (GPU) model clip by clip
-        video = video.cpu().numpy()
 
     segmentations = segment_a_video_with_fusion(video, model=model, interpolate_last=True, step=args.step,
                                                 num_clips=args.fuse, fuse_method=args.fuse_method, class_list=[0, 1],
-                                                batch_size=args.batch_size)
+                                                batch_size=args.batch_size,
+                                                strict_reference=not args.no_strict_reference)
     predicted_efs, edes_pairs = compute_ef_using_putative_clips(segmentations, test_pat_index=args.path,
                                                                 return_edes=True)
     if args.verbose:

@@ -144,6 +144,18 @@ def majority_vote(votes, class_list=(0, 1)):
     return np.asarray(class_list)[np.argmax(counts, axis=0)].astype(np.uint8)
 
 
+def itk_voting(votes, class_list=(0, 1)):
+    """itk::LabelVotingImageFilter with the default undecided label (max input label + 1): plurality,
+    a tie of the top counts -> undecided. PARITY UNPINNED (SimpleITK / LabelFusion absent)."""
+    v = np.stack(votes).astype(np.int64)
+    counts = np.stack([(v == c).sum(0) for c in class_list])
+    top = counts.max(0)
+    winners = (counts == top[None]).sum(0)
+    undecided = int(v.max()) + 1
+    out = np.asarray(class_list)[np.argmax(counts, axis=0)]
+    return np.where(winners > 1, undecided, out).astype(np.uint8)
+
+
 def _dice(a, b):
     s = a.sum() + b.sum()
     return 1.0 if s == 0 else 2.0 * float((a & b).sum()) / float(s)
@@ -222,7 +234,7 @@ def _weighted_mv(cands, w):
 
 
 FUSERS = {"majority": majority_vote, "majorityvoting": majority_vote, "mv": majority_vote,
-          "itkvoting": majority_vote, "simple": simple_vote, "staple": staple_vote}
+          "itkvoting": itk_voting, "voting": itk_voting, "simple": simple_vote, "staple": staple_vote}
 
 
 def fuse_frames(passes, t, step, fuse_method="simple", class_list=(0, 1)):

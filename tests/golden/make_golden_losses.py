@@ -35,6 +35,11 @@ def loss_inputs(T=6, H=32, W=40, seed=17):
                 warp_img=warp_img, warp_motion=warp_motion, warp_gout=warp_gout)
 
 
+# extra motion_seg_loss cases (ed_index, es_index, start, end): ES before ED, and a window that
+# starts after the seed frames (the reference's forward loops ignore `start`, its backward loops `end`)
+SGS_CASES = [(4, 1, 0, 6), (1, 4, 2, 6), (0, 3, 1, 5), (3, 2, 2, 4)]
+
+
 def main():
     from tests.golden.make_golden import REF, install_stubs
     install_stubs()
@@ -62,6 +67,18 @@ def main():
     out["sgs_ots_loss"] = np.float64(ots.item())
     out["sgs_grad_motion"] = motion.grad.numpy()
     out["sgs_grad_logits"] = logits.grad.numpy()
+
+    for i, (ed_i, es_i, start, end) in enumerate(SGS_CASES):
+        motion = torch.from_numpy(d["motion"]).requires_grad_()
+        logits = torch.from_numpy(d["logits"]).requires_grad_()
+        flow, ots = motion_seg_loss(d["ed"], d["es"], ed_i, es_i, motion, F.softmax(logits, dim=1), start=start, end=end)
+        total = flow + ots
+        if torch.is_tensor(total) and total.requires_grad:
+            total.backward()
+        out[f"sgs{i}_flow_loss"] = np.float64(float(flow))
+        out[f"sgs{i}_ots_loss"] = np.float64(float(ots))
+        out[f"sgs{i}_grad_motion"] = motion.grad.numpy() if motion.grad is not None else np.zeros_like(d["motion"])
+        out[f"sgs{i}_grad_logits"] = logits.grad.numpy() if logits.grad is not None else np.zeros_like(d["logits"])
 
     img = torch.from_numpy(d["warp_img"]).requires_grad_()
     mot = torch.from_numpy(d["warp_motion"]).requires_grad_()

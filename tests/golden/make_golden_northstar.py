@@ -1,8 +1,9 @@
 """Generate tests/golden/northstar_c1.npz: the CPU reference path at BASELINE config[1].
 
 One 200-frame synthetic EchoNet-style video (synthetic.echo_video(200, seed=0), zero-one normalised),
-5 temporally shifted passes with step 1 (30 clips of 32 frames), the seeded synthetic weights
-(weights.synthetic_state_dict(DEFAULT_SEED)) -- exactly bench.py's per-GPU workload. Everything is
+5 temporally shifted passes with step 1 (30 clips of 32 frames), the seeded "echo" weights
+(weights.echo_state_dict(DEFAULT_SEED): the segmentation follows the synthetic LV, so the EFs are
+physiological, ~76 %) -- exactly bench.py's per-GPU workload. Everything is
 computed by the oracle (tests-only infrastructure): the torch-CPU restatement of the reference model
 (oracle/r2plus1d_ref.py, pinned to the reference module by tests/golden/model_forward.npz) and the
 numpy restatement of src/fuse_utils.py (oracle/fuse_ref.py, pinned by tests/golden/plumbing.npz).
@@ -29,6 +30,7 @@ sys.path.insert(0, REPO)
 from oracle import fuse_ref, r2plus1d_ref  # noqa: E402
 
 T, F, STEP, SEED = 200, 5, 1, 0
+RECIPE = "echo"
 METHODS = ("majority", "simple", "staple")
 
 
@@ -37,7 +39,7 @@ def main():
     import clasfv_amd.weights as W
     from clasfv_amd.echo import compute_ef_using_putative_clips
     torch.set_num_threads(os.cpu_count() or 8)
-    sd = W.synthetic_state_dict(W.DEFAULT_SEED)
+    sd = W.recipe_state_dict(RECIPE, W.DEFAULT_SEED)
     model = r2plus1d_ref.OracleModel(sd)
     video = fuse_ref.zeroone_normalizer(S.echo_video(T, seed=SEED))
     k = fuse_ref.clamp_num_clips(T, F, STEP)
@@ -54,7 +56,7 @@ def main():
     print(f"{sum(len(range(0, fuse_ref.n_clip_frames(T - s), 32)) for s in range(k))} clip forwards "
           f"in {time.time() - t0:.1f} s")
     out = {"T": np.int64(T), "fuse": np.int64(F), "step": np.int64(STEP), "seed": np.int64(SEED),
-           "weights_seed": np.int64(W.DEFAULT_SEED),
+           "weights_seed": np.int64(W.DEFAULT_SEED), "weights_recipe": np.array(RECIPE),
            "passes": np.packbits(np.concatenate([p.ravel() for p in passes]).astype(np.uint8)),
            "pass_frames": np.array([p.shape[0] for p in passes], np.int64)}
     m = np.concatenate(margins)

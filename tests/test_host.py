@@ -32,10 +32,18 @@ def test_library_builds_and_exports_every_header_symbol():
     assert set(funcs) == set(_lib.SIGNATURES), "ctypes signatures out of sync with include/clasfv.h"
 
 
+def test_abi_version_matches_header():
+    from clasfv_amd import _lib
+    m = re.search(r"#define CLASFV_ABI_VERSION (\d+)", open(HEADER).read())
+    assert m and int(m.group(1)) == _lib.ABI_VERSION == _lib.load().clasfv_version()
+    bits = dict(re.findall(r"CLASFV_VARIANT_(\w+) = (\d+)", open(HEADER).read()))
+    assert {k.lower(): int(v) for k, v in bits.items()} == _lib.VARIANTS
+
+
 def test_library_reports_errors_without_gpu():
     from clasfv_amd import _lib
     lib = _lib.load()
-    assert lib.clasfv_version() == 1
+    assert lib.clasfv_version() == _lib.ABI_VERSION
     if torch.cuda.is_available():
         pytest.skip("GPU present")
     h = ctypes.c_void_p()
@@ -268,3 +276,68 @@ def test_fast_division_magic_numbers(tmp_path):
     hdr = open(os.path.join(REPO, "fully-automated-multi-heartbeat-echocardiography-video-segmentation-and-motion-tracking_amd",
                             "csrc", "common.h")).read()
     assert "(((1ull << 32) * ((1ull << l) - d)) / d + 1)" in hdr  # the construction the check restates
+
+
+def test_strict_reference_clamp_and_frames():
+    """src/fuse_utils.py:38-42 clamps T in [32, 32 + step) to K = 0 (then IndexError at :82);
+    strict_reference=False runs one pass there, and keeps all T frames for step > 1 (:85)."""
+    from clasfv_amd import fuse_utils as FU
+    assert FU.clamp_num_clips(32, 1, 1) == 0 and FU.clamp_num_clips(32, 1, 1, strict_reference=False) == 1
+    assert FU.clamp_num_clips(34, 5, 3) == 0 and FU.clamp_num_clips(34, 5, 3, strict_reference=False) == 1
+    assert FU.clamp_num_clips(200, 5, 1, strict_reference=False) == 5
+    assert FU.fused_frames(80, 2) == 79 and FU.fused_frames(80, 2, strict_reference=False) == 80
+    labels = torch.arange(3 * 6, dtype=torch.uint8).view(3, 6, 1, 1)  # 3 passes x 6 frames
+    fused = torch.tensor([100, 101, 102, 103], dtype=torch.uint8).view(4, 1, 1)  # frames 0, 3, 4, 5
+    got = FU.keep_dropped_frames(labels, fused, 3).view(-1).tolist()
+    assert got == [100, 1, 2, 101, 102, 103]
+
+
+def test_config2_plan_videos_per_rank_and_no_exchange():
+    """BASELINE config[2]: 64 x 200-frame videos over 8 ranks (f = 1 and f = 5): every rank holds
+    exactly its 8 videos and no clip crosses ranks."""
+    from clasfv_amd.dist import exchange_stats, videos_needed
+    lengths = [200] * 64
+    for f in (1, 5):
+        for world in (1, 2, 4, 8):
+            need = [videos_needed(lengths, f, 1, r, world) for r in range(world)]
+            assert [len(n) for n in need] == [64 // world] * world
+            assert sorted(sum(need, [])) == list(range(64))
+            assert exchange_stats(lengths, f, 1, world) == (0, 0)
+    rows, nbytes = exchange_stats([70, 96, 45], 3, 1, 2)
+    assert rows > 0 and nbytes == rows * 32 * 112 * 112 * 4
+
+
+def test_bench_rejects_world_size_mismatch():
+    """bench.py under a launcher: WORLD_SIZE must equal --gpus (checked before any GPU call)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1"], capture_output=True, text=True, timeout=120,
+                       cwd=REPO, env=env)
+    assert r.returncode != 0 and "must agree" in r.stderr
+
+
+def test_itk_voting_oracle_rule():
+    from oracle import fuse_ref
+    a = np.array([[0, 1], [1, 1]], np.uint8)
+    b = np.array([[0, 0], [1, 0]], np.uint8)
+    c = np.array([[1, 0], [1, 1]], np.uint8)
+    np.testing.assert_array_equal(fuse_ref.itk_voting([a, b]), [[0, 2], [1, 2]])  # ties -> undecided (max + 1)
+    np.testing.assert_array_equal(fuse_ref.itk_voting([a, b, c]), [[0, 0], [1, 1]])
+    np.testing.assert_array_equal(fuse_ref.majority_vote([a, b]), [[0, 0], [1, 0]])
+
+
+def test_echo_weights_keep_the_random_recipe_elsewhere():
+    """The "echo" recipe changes only its designed units; every other weight is the random recipe's."""
+    import clasfv_amd.weights as W
+    r, e = W.synthetic_state_dict(1234), W.echo_state_dict(1234)
+    assert list(r) == list(e)
+    same = [k for k in r if np.array_equal(r[k], e[k])]
+    assert len(same) > 150
+    for k in ("r2plus1d_model.layer2.0.conv1.0.0.weight", "r2plus1d_model.layer4.1.conv2.0.3.weight"):
+        assert np.array_equal(r[k], e[k])
+    w = e["r2plus1d_model.stem.0.weight"]
+    assert np.array_equal(w[6:], r["r2plus1d_model.stem.0.weight"][6:])
+    assert np.allclose(w[0].sum(), W.ECHO["S0"])  # box mean of the intensity
+    w1 = e["comb_1_layer.weight"].reshape(64, 1024)
+    assert np.array_equal(w1[7:], r["comb_1_layer.weight"].reshape(64, 1024)[7:])

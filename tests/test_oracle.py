@@ -198,3 +198,15 @@ def test_staple_restatement_known_answers():
     assert (out != truth).mean() < 0.01
     assert np.array_equal(fuse_ref.staple_vote([np.zeros((5, 5), np.uint8)] * 2), np.zeros((5, 5), np.uint8))
     assert np.array_equal(fuse_ref.staple_vote([np.ones((5, 5), np.uint8)] * 2), np.ones((5, 5), np.uint8))
+
+
+def test_northstar_fixture_is_physiological():
+    """tests/golden/northstar_c1.npz (the CPU path on config[1] with the "echo" weights): the masks
+    follow the synthetic LV, so the EFs are physiological and the ED/ES pairs are the video's cycles
+    (period 50) -- the EF leg of the north_star bar is not degenerate."""
+    g = golden("northstar_c1.npz")
+    assert str(g["weights_recipe"]) == "echo"
+    for m in ("majority", "simple", "staple"):
+        efs = g[f"ef_{m}"]
+        assert len(efs) == 4 and np.all((30 < efs) & (efs < 80)), efs
+        assert g[f"pairs_{m}"].tolist() == [[0, 25], [50, 75], [100, 125], [150, 175]]

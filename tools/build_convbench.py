@@ -10,16 +10,18 @@ REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 import clasfv_amd.build as B  # noqa: E402
 
-KERNELS = ["winograd.hip", "winograd2.hip", "winograd3.hip", "winograd_t.hip", "winograd_w.hip", "conv.hip", "conv_patch.hip",
-           "decoder.hip"]
+KERNELS = ["winograd.hip", "winograd2.hip", "winograd_t.hip", "conv.hip", "conv_patch.hip", "decoder.hip"]
+# measured-slower design points kept out of the product library
+EXPERIMENTAL = ["winograd3.hip", "winograd_w.hip"]
 
 
 def main():
     out = os.path.join(HERE, "bin")
     os.makedirs(os.path.join(out, "obj"), exist_ok=True)
     hipcc = B._hipcc()
-    flags = [f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-DCLASFV_KNOCKOUTS", "-I", B.INCLUDE]
+    flags = [f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-DCLASFV_KNOCKOUTS", "-I", B.INCLUDE, "-I", B.CSRC]
     jobs = [(os.path.join(B.CSRC, f), B.EXTRA_FLAGS.get(f, [])) for f in KERNELS]
+    jobs += [(os.path.join(HERE, "experimental", f), []) for f in EXPERIMENTAL]
     jobs.append((os.path.join(HERE, "convbench.hip"), []))
     jobs.append((os.path.join(HERE, "conv_patch_v1.hip"), []))
     jobs.append((os.path.join(HERE, "winoq_probe.hip"), []))
