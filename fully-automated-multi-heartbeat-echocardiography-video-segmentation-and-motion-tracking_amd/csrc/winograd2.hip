@@ -423,9 +423,13 @@ hipError_t launch_winoq(const ConvParams& p, hipStream_t s) {
 }
 
 #ifdef CLASFV_KNOCKOUTS
-// tools/convbench.hip: the product dispatch
+// tools/convbench.hip: ko 0 = conv_wino_q, 7 = conv_wino_s (tools/experimental/winograd_s.hip), 8.. = its
+// timing variants
+hipError_t launch_winos(const ConvParams& p, hipStream_t s);
+hipError_t launch_winos_var(const ConvParams& p, hipStream_t s, int var);
 hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko) {
-  (void)ko;
+  if (ko == 7) return launch_winos(p, s);
+  if (ko >= 8) return launch_winos_var(p, s, ko - 8);  // ko = 8 + VAR (12: stamps; 20, 28, 36, 44: knock-outs)
   return launch_winoq(p, s);
 }
 #endif

@@ -23,6 +23,7 @@ hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
 hipError_t launch_patch_bf16_v1(const ConvParams& p, hipStream_t s);
 hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winoq_probe(const ConvParams& p, hipStream_t s, int ko);
+void winos_stamps(unsigned long long* out);
 
 // decoder: N clips of T x H x W, taps at (T, H/2, W/2), (T/2, H/4, W/4), (T/4, H/8), (T/8, H/16)
 static int run_decoder(int N, int T, int H, int W, int iters, const std::vector<int>& kos);
@@ -154,6 +155,20 @@ int main(int argc, char** argv) {
       ms /= iters;
       if (ms < best[v]) best[v] = ms;
     }
+  if (winoq)
+    for (int ko : kos)
+      if (ko == 12 || ko == 20 || ko == 28 || ko == 36 || ko == 44) {  // conv_wino_s stamps: per block, consumer / producer wait + barrier vs total cycles
+        CK(hipDeviceSynchronize());
+        launch(ko);  // the stamps of this variant
+        CK(hipDeviceSynchronize());
+        unsigned long long st[8][2][2];
+        winos_stamps(&st[0][0][0]);
+        printf("ko %d\n", ko);
+        for (int bl = 0; bl < 8; ++bl)
+          printf("stamps block %d: consumer wait %llu / %llu (%.3f), producer wait %llu / %llu (%.3f)\n", bl,
+                 st[bl][0][0], st[bl][0][1], st[bl][0][1] ? (double)st[bl][0][0] / st[bl][0][1] : 0.0, st[bl][1][0],
+                 st[bl][1][1], st[bl][1][1] ? (double)st[bl][1][0] / st[bl][1][1] : 0.0);
+      }
   for (size_t v = 0; v < kos.size(); ++v)
     printf("%s%s%-6s N=%d T=%d H=%d W=%d Cin=%d Cout=%d ko=%-3d  %8.3f ms  %7.1f TF(alg)\n", p.res ? "res   " : "nores ", bf ? "bf16 " : "",
            kind, N, T, H, W, Cin, Cout, kos[v], best[v], gflop / best[v]);

@@ -27,6 +27,10 @@
 //   uniform vmcnt(2) at the next interval covers both (store counts differ between producer waves).
 #include "common.h"
 
+// (declarations the product header no longer carries: this kernel is an experiment, tools/ only)
+bool winos_supported(const ConvParams& p);
+hipError_t launch_winos(const ConvParams& p, hipStream_t s);
+
 namespace {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -51,8 +55,16 @@ struct Item {
   int pair, n0;  // patch pair index (patches 2 pair, 2 pair + 1) and first output channel
 };
 
-// EPI: bit 0 residual add, bit 1 ReLU; C8: 8-channel-blocked output (see conv_wino_q)
-template <int NCH, int EPI, bool C8>
+#ifdef CLASFV_KNOCKOUTS
+// diagnostic stamps (tools/convbench.hip, VAR bit 2): per block < 8, per role, cycles spent in the
+// per-chunk wait + barrier and in total (lane 0 of waves 0 and 4)
+__device__ unsigned long long g_wstamps[8][2][2];
+#endif
+
+// EPI: bit 0 residual add, bit 1 ReLU; C8: 8-channel-blocked output (see conv_wino_q). VAR (timing
+// experiments only, 0 in the product): bit 0 consumer priority, bit 1 no producer priority, bit 2 stamps;
+// knock-outs (wrong results, timing only): bit 3 no epilogue, bit 4 no transform, bit 5 no MFMAs.
+template <int NCH, int EPI, bool C8, int VAR = 0>
 __global__ __launch_bounds__(512) void conv_wino_s(ConvParams p, int n_co, int n_patches, int n_pairs,
                                                     FastDiv fd_co, FastDiv fd_frame, FastDiv fd_px) {
   static_assert(NCH >= 4, "the DMA stream runs 4 chunks ahead within one item boundary");
@@ -80,7 +92,19 @@ __global__ __launch_bounds__(512) void conv_wino_s(ConvParams p, int n_co, int n
     return Item{pair_lo + pi, (t - pi * n_co) * 48};
   };
 
-  if (consumer) __builtin_amdgcn_s_setprio(1);
+  // the producers' latency chains, not the consumers' MFMA stream, set the interval length
+  // (tools/gpu_winos_b.sh stamps): the producers get the issue priority
+  if ((VAR & 1) && consumer) __builtin_amdgcn_s_setprio(1);
+  if (!(VAR & 2) && !consumer) __builtin_amdgcn_s_setprio(1);
+  unsigned long long st_wait = 0, st_t0 = 0;
+  if constexpr ((VAR & 4) != 0) st_t0 = __builtin_amdgcn_s_memtime();
+  auto stamp_wait = [&](unsigned long long a) __attribute__((always_inline)) {
+    if constexpr ((VAR & 4) != 0) st_wait += __builtin_amdgcn_s_memtime() - a;
+  };
+  auto now = [&]() __attribute__((always_inline)) -> unsigned long long {
+    if constexpr ((VAR & 4) != 0) return __builtin_amdgcn_s_memtime();
+    return 0;
+  };
 
   // ---- consumer state --------------------------------------------------------------------------
   const int q = lane >> 4, l16 = lane & 15;
@@ -140,13 +164,16 @@ __global__ __launch_bounds__(512) void conv_wino_s(ConvParams p, int n_co, int n
   const int cc = ptid & 7;
   const int raw_off = (tt / 16) * S_PSTRIDE * 8 + (2 * ((tt / 4) % 4) * S_SIDE + 2 * (tt % 4)) * 8 + cc;
   const int v_off = (((tt & 15) * 4 + ((cc >> 1) ^ (((tt & 15) >> 2) & 2))) * 2 + (tt >> 4)) * 2 + (cc & 1);
-  auto transform = [&](int rstage, int vstage) __attribute__((always_inline)) {
+  // transform split in two so the LDS read latency overlaps other producer work: read the 4x4 window
+  // of raw(s+2) right after the barrier, compute and store V later in the interval
+  auto transform_read = [&](int rstage, float (&d)[16]) __attribute__((always_inline)) {
     const float* rb = reinterpret_cast<const float*>(raw + rstage * S_RAW) + raw_off;
-    float d[16];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int c = 0; c < 4; ++c) d[4 * r + c] = rb[(r * S_SIDE + c) * 8];
+  };
+  auto transform_write = [&](const float (&d)[16], int vstage) __attribute__((always_inline)) {
     float t[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -164,39 +191,60 @@ __global__ __launch_bounds__(512) void conv_wino_s(ConvParams p, int n_co, int n
       vb[(4 * r + 3) * S_BT * 8] = t[4 * r + 1] - t[4 * r + 3];
     }
   };
-  // epilogue of item t by the producers: unit = (tile, 4 channels), conv_wino_q's arithmetic
+  auto transform = [&](int rstage, int vstage) __attribute__((always_inline)) {
+    float d[16];
+    transform_read(rstage, d);
+    transform_write(d, vstage);
+  };
+  // epilogue of item t by the producers: unit = (tile, 4 channels), conv_wino_q's arithmetic. Split in
+  // two: epi_prepare (one interval ahead: output offsets, bias and residual loads in flight) and
+  // epi_finish (Z rows -> output transform -> bias / residual / ReLU -> stores).
   constexpr int CQ = 12, UNITS = S_BT * CQ, UPT = (UNITS + 255) / 256;
   constexpr bool RES = EPI & 1, RELU = EPI & 2;
   const float* res = reinterpret_cast<const float*>(p.res);
   float* yout = reinterpret_cast<float*>(p.y);
   const int ps = C8 ? 8 : CO;
   const size_t oplane = (size_t)n_patches * 64 * 8;
-  auto epilogue = [&](int t) __attribute__((always_inline)) {
-    if (t < 0 || t >= n_items) return;
-    const Item it = item_of(t);
-#pragma unroll
-    for (int u = 0; u < UPT; ++u) {
+  struct Epi {
+    size_t o[UPT];
+    int zo[UPT];
+    bool live[UPT];
+    f32x4 bias[UPT];
+    f32x4 rr[UPT][RES ? 4 : 1];
+  };
+  // one unit per call (u: compile-time): the epilogue is spread over two intervals per side
+  auto epi_prepare = [&](int t, Epi& e, int u) __attribute__((always_inline)) {
+    const bool item_live = t >= 0 && t < n_items;
+    const Item it = item_of(item_live ? t : 0);
+    {
       const int un = ptid + 256 * u;
       const int tl = C8 ? un % S_BT : un / CQ, cq = C8 ? un / S_BT : un - tl * CQ;
       const int gp = 2 * it.pair + tl / 16;
-      if (un >= UNITS || gp >= n_patches) continue;
-      const int f = fdiv(gp, fd_frame), r = gp - f * (PY * PX);
+      const bool live = item_live && un < UNITS && gp < n_patches;
+      const int gpc = live ? gp : 0;
+      const int f = fdiv(gpc, fd_frame), r = gpc - f * (PY * PX);
       const int pr = fdiv(r, fd_px), pc = r - pr * PX;
       const int yy = pr * 8 + 2 * ((tl / 4) % 4), xx = pc * 8 + 2 * (tl % 4);
-      const int co = it.n0 + 4 * cq;
+      const int co = live ? it.n0 + 4 * cq : 0;
       const size_t pix = (size_t)(f * H + yy) * W + xx;
-      const size_t o = C8 ? (co >> 3) * oplane + pix * 8 + (co & 7) : pix * CO + co;
-      const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 rr[4];
+      e.o[u] = C8 ? (co >> 3) * oplane + pix * 8 + (co & 7) : pix * CO + co;
+      e.zo[u] = tl * 48 + 4 * cq;
+      e.live[u] = live;
+      e.bias[u] = (p.bias && live) ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (RES) {
 #pragma unroll
-      for (int px = 0; px < 4; ++px)
-        rr[px] = RES ? *reinterpret_cast<const f32x4*>(res + o + (size_t)((px >> 1) * W + (px & 1)) * ps)
-                     : f32x4{0.f, 0.f, 0.f, 0.f};
-      const int zo = tl * 48 + 4 * cq;
+        for (int px = 0; px < 4; ++px)
+          e.rr[u][px] = live ? *reinterpret_cast<const f32x4*>(res + e.o[u] + (size_t)((px >> 1) * W + (px & 1)) * ps)
+                             : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  auto epi_finish = [&](const Epi& e, int u) __attribute__((always_inline)) {
+    if (e.live[u]) {
       f32x4 z[4][2];
 #pragma unroll
       for (int i2 = 0; i2 < 4; ++i2) {
-        const f32x4* zp = reinterpret_cast<const f32x4*>(zs + i2 * S_BT * 48 + zo);
+        const f32x4* zp = reinterpret_cast<const f32x4*>(zs + i2 * S_BT * 48 + e.zo[u]);
         z[i2][0] = zp[0];
         z[i2][1] = zp[1];
       }
@@ -207,14 +255,14 @@ __global__ __launch_bounds__(512) void conv_wino_s(ConvParams p, int n_co, int n
           f32x4 v;
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            const int h = c >> 1, e = (c & 1) * 2 + b2;
-            const float y = a2 == 0 ? z[0][h][e] + z[1][h][e] + z[2][h][e] : z[1][h][e] - z[2][h][e] - z[3][h][e];
-            float o2 = y + bias[c];
-            if constexpr (RES) o2 += rr[2 * a2 + b2][c];
+            const int h = c >> 1, ee = (c & 1) * 2 + b2;
+            const float y = a2 == 0 ? z[0][h][ee] + z[1][h][ee] + z[2][h][ee] : z[1][h][ee] - z[2][h][ee] - z[3][h][ee];
+            float o2 = y + e.bias[u][c];
+            if constexpr (RES) o2 += e.rr[u][2 * a2 + b2][c];
             if constexpr (RELU) o2 = fmaxf(o2, 0.f);
             v[c] = o2;
           }
-          *reinterpret_cast<f32x4*>(yout + o + (size_t)(a2 * W + b2) * ps) = v;
+          *reinterpret_cast<f32x4*>(yout + e.o[u] + (size_t)(a2 * W + b2) * ps) = v;
         }
     }
   };
@@ -237,13 +285,16 @@ __global__ __launch_bounds__(512) void conv_wino_s(ConvParams p, int n_co, int n
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
         __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long w0 = now();
         __builtin_amdgcn_s_waitcnt(0x0070 | 6);  // U(s) landed (U(s+1) in flight); lgkmcnt(0): A(s), Z stores
         __builtin_amdgcn_s_barrier();
+        stamp_wait(w0);
         __builtin_amdgcn_sched_barrier(0);  // nothing (MFMAs included) moves across an interval boundary
         const int s = t * NCH + k;  // chunk position in the block's stream
         read_a((s + 1) % 3, aa[(k + 1) & 1]);
         f32x4(&ac)[4] = aa[k & 1];
         f32x4(&uc)[3][2] = uu[k & 1];
+        if (!(VAR & 32))
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -277,6 +328,14 @@ __global__ __launch_bounds__(512) void conv_wino_s(ConvParams p, int n_co, int n
     __builtin_amdgcn_s_waitcnt(0xC07F);  // Z stores
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_waitcnt(0x0070);  // past-the-end U loads
+#ifdef CLASFV_KNOCKOUTS
+    if constexpr ((VAR & 4) != 0) {
+      if (blockIdx.x < 8 && wid == 0 && lane == 0) {
+        g_wstamps[blockIdx.x][0][0] = st_wait;
+        g_wstamps[blockIdx.x][0][1] = __builtin_amdgcn_s_memtime() - st_t0;
+      }
+    }
+#endif
   } else {
     // prologue: raw(0..2) in flight, transform raw(0) and raw(1), raw(3) in flight
     dma_offsets(0);
@@ -292,41 +351,65 @@ __global__ __launch_bounds__(512) void conv_wino_s(ConvParams p, int n_co, int n
     transform(1, 1);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // own V stores done
     __builtin_amdgcn_s_barrier();
+    Epi ep;
+#pragma unroll
+    for (int u = 0; u < UPT; ++u) epi_prepare(-1, ep, u);  // no item before the first: every unit dead
     for (int t = 0; t < n_items; ++t) {
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
-        // raw(s+2) landed (raw(s+3) in flight; older epilogue stores done too); own V stores done
+        // raw(s+2) landed (raw(s+3) in flight; the previous interval's epilogue loads / stores, issued
+        // before its DMAs, done too); own V stores done
         __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long w0 = now();
         __builtin_amdgcn_s_waitcnt(0x0070 | S_DPW);
         __builtin_amdgcn_s_barrier();
+        stamp_wait(w0);
         __builtin_amdgcn_sched_barrier(0);
         const int s = t * NCH + k;
-        if (k == 0) epilogue(t - 1);
+        float d[16];
+        if (!(VAR & 16)) transform_read((s + 2) % 3, d);  // in flight during the epilogue below
+        if (!(VAR & 8)) {
+          // item t-1 (its Z rows landed before the k = 0 barrier), one unit per interval
+          if (k < UPT && t > 0) epi_finish(ep, k);
+          // item t: offsets, bias, residual in flight, one unit per interval
+          if (k >= NCH - UPT) epi_prepare(t, ep, k - (NCH - UPT));
+        }
         // raw(s+4): chunk k+4 of this item or chunk k+4-NCH of the next (offsets switch at k = NCH-4)
         if (k == NCH - 4) dma_offsets(t + 1);
         issue_raw(k + 4 < NCH ? k + 4 : k + 4 - NCH, (s + 4) % 3);
-        transform((s + 2) % 3, (s + 2) % 3);
+        if (!(VAR & 16)) transform_write(d, (s + 2) % 3);
       }
     }
     // drain: the last item's epilogue (its Z rows were written in the last interval)
     __builtin_amdgcn_s_waitcnt(0x0070);
     __builtin_amdgcn_s_barrier();
-    epilogue(n_items - 1);
+    if (!(VAR & 8)) {
+#pragma unroll
+      for (int u = 0; u < UPT; ++u) epi_finish(ep, u);
+    }
     __builtin_amdgcn_s_waitcnt(0x0070);  // every DMA (past-the-end fetches included) landed before exit
+#ifdef CLASFV_KNOCKOUTS
+    if constexpr ((VAR & 4) != 0) {
+      if (blockIdx.x < 8 && wid == 4 && lane == 0) {
+        g_wstamps[blockIdx.x][1][0] = st_wait;
+        g_wstamps[blockIdx.x][1][1] = __builtin_amdgcn_s_memtime() - st_t0;
+      }
+    }
+#endif
   }
 }
 
-template <int NCH, int EPI, bool C8>
+template <int NCH, int EPI, bool C8, int VAR = 0>
 hipError_t launch_s(const ConvParams& p, hipStream_t s, int grid, int n_co, int n_patches, int n_pairs) {
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_wino_s<NCH, EPI, C8>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_wino_s<NCH, EPI, C8, VAR>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, S_LDS);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const int px = p.Wo / 8, py = p.Ho / 8;
-  hipLaunchKernelGGL((conv_wino_s<NCH, EPI, C8>), dim3(grid), dim3(512), S_LDS, s, p, n_co, n_patches, n_pairs,
+  hipLaunchKernelGGL((conv_wino_s<NCH, EPI, C8, VAR>), dim3(grid), dim3(512), S_LDS, s, p, n_co, n_patches, n_pairs,
                      fast_div(n_co), fast_div(px * py), fast_div(px));
   return hipGetLastError();
 }
@@ -370,3 +453,34 @@ hipError_t launch_winos(const ConvParams& p, hipStream_t s) {
   return p.Cin == 64 ? launch_s_epi<8>(p, s, grid, n_co, n_patches, n_pairs)
                      : launch_s_epi<16>(p, s, grid, n_co, n_patches, n_pairs);
 }
+
+#ifdef CLASFV_KNOCKOUTS
+// tools/convbench.hip: VAR variants of the layer1 shape (Cin 64, no residual / residual + ReLU, channels-last)
+hipError_t launch_winos_var(const ConvParams& p, hipStream_t s, int var) {
+  if (!winos_supported(p) || p.Cin != 64 || p.y_c8) return hipErrorInvalidValue;
+  const int n_patches = p.N * p.To * (p.Ho / 8) * (p.Wo / 8);
+  const int n_pairs = (n_patches + 1) / 2;
+  const int n_co = p.Cout / 48;
+  const int grid = n_pairs < cu_count() ? n_pairs : cu_count();
+  const bool res = p.res != nullptr;
+#define VARCASE(V)                                                                                  \
+  case V:                                                                                           \
+    return res ? launch_s<8, 3, false, V>(p, s, grid, n_co, n_patches, n_pairs)                      \
+               : launch_s<8, 2, false, V>(p, s, grid, n_co, n_patches, n_pairs);
+  switch (var) {
+    VARCASE(0)
+    VARCASE(1)
+    VARCASE(2)
+    VARCASE(3)
+    VARCASE(4)
+    VARCASE(12)
+    VARCASE(20)
+    VARCASE(28)
+    VARCASE(36)
+  }
+#undef VARCASE
+  return hipErrorInvalidValue;
+}
+
+void winos_stamps(unsigned long long* out) { (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), sizeof(g_wstamps)); }
+#endif
