@@ -157,7 +157,7 @@ int main(int argc, char** argv) {
     }
   if (winoq)
     for (int ko : kos)
-      if (ko == 12 || ko == 20 || ko == 28 || ko == 36 || ko == 44) {  // conv_wino_s stamps: per block, consumer / producer wait + barrier vs total cycles
+      if (ko == 12 || ko == 20 || ko == 28 || ko == 36 || ko == 44 || ko == 76 || ko == 100) {  // conv_wino_s stamps: per block, consumer / producer wait + barrier vs total cycles
         CK(hipDeviceSynchronize());
         launch(ko);  // the stamps of this variant
         CK(hipDeviceSynchronize());
@@ -223,11 +223,33 @@ static int run_decoder(int N, int T, int H, int W, int iters, const std::vector<
   CK(hipMalloc((void**)&d.seg, (size_t)N * 2 * T * H * W * 4));
   CK(hipMalloc((void**)&d.mot, (size_t)N * 4 * T * H * W * 4));
   d.N = N, d.T = T, d.H = H, d.W = W;
+  d.bf16 = getenv("CB_BF16") ? 1 : 0;
   hipStream_t s;
   CK(hipStreamCreate(&s));
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
+  // outputs of every variant against the first one's (seg logits and tanh(motion))
+  const size_t nseg = (size_t)N * 2 * T * H * W, nmot = (size_t)N * 4 * T * H * W;
+  std::vector<float> ref(nseg + nmot), got(nseg + nmot);
+  for (size_t v = 0; v < kos.size(); ++v) {
+    CK(hipMemset(d.seg, 0, nseg * 4));
+    CK(hipMemset(d.mot, 0, nmot * 4));
+    CK(launch_decoder_ko(d, s, kos[v]));
+    CK(hipStreamSynchronize(s));
+    std::vector<float>& o = v ? got : ref;
+    CK(hipMemcpy(o.data(), d.seg, nseg * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(o.data() + nseg, d.mot, nmot * 4, hipMemcpyDeviceToHost));
+    if (!v) continue;
+    size_t nd = 0;
+    double md = 0;
+    for (size_t i = 0; i < o.size(); ++i)
+      if (memcmp(&ref[i], &got[i], 4)) {
+        ++nd;
+        md = fmax(md, fabs((double)ref[i] - got[i]));
+      }
+    printf("check dec ko=%d vs ko=%d: %zu of %zu differ, max |diff| %.3e\n", kos[v], kos[0], nd, o.size(), md);
+  }
   for (int ko : kos)
     for (int i = 0; i < 5; ++i) CK(launch_decoder_ko(d, s, ko));
   std::vector<float> best(kos.size(), 1e30f);

@@ -63,7 +63,8 @@ __device__ unsigned long long g_wstamps[8][2][2];
 
 // EPI: bit 0 residual add, bit 1 ReLU; C8: 8-channel-blocked output (see conv_wino_q). VAR (timing
 // experiments only, 0 in the product): bit 0 consumer priority, bit 1 no producer priority, bit 2 stamps;
-// knock-outs (wrong results, timing only): bit 3 no epilogue, bit 4 no transform, bit 5 no MFMAs.
+// knock-outs (wrong results, timing only): bit 3 no epilogue, bit 4 no transform, bit 5 no MFMAs,
+// bit 6 no U loads in the chunk loop (stale U registers).
 template <int NCH, int EPI, bool C8, int VAR = 0>
 __global__ __launch_bounds__(512) void conv_wino_s(ConvParams p, int n_co, int n_patches, int n_pairs,
                                                     FastDiv fd_co, FastDiv fd_frame, FastDiv fd_px) {
@@ -308,10 +309,12 @@ __global__ __launch_bounds__(512) void conv_wino_s(ConvParams p, int n_co, int n
                                                                      c0, 0, 0, 0);
               }
         // U(s+2) into the registers chunk s just consumed: chunk k+2 of this item or k+2-NCH of the next
-        if (k + 2 < NCH)
-          load_u(k + 2, itc.n0, uu[k & 1]);
-        else
-          load_u(k + 2 - NCH, itn.n0, uu[k & 1]);
+        if constexpr ((VAR & 64) == 0) {
+          if (k + 2 < NCH)
+            load_u(k + 2, itc.n0, uu[k & 1]);
+          else
+            load_u(k + 2 - NCH, itn.n0, uu[k & 1]);
+        }
         if (k == NCH - 1) {  // hand the item's accumulators to the producers
 #pragma unroll
           for (int m = 0; m < 2; ++m)
@@ -477,6 +480,10 @@ hipError_t launch_winos_var(const ConvParams& p, hipStream_t s, int var) {
     VARCASE(20)
     VARCASE(28)
     VARCASE(36)
+    VARCASE(64)
+    VARCASE(68)
+    VARCASE(88)
+    VARCASE(92)
   }
 #undef VARCASE
   return hipErrorInvalidValue;
