@@ -50,6 +50,11 @@ struct ConvParams {
   // environment once at clasfv_create or set with clasfv_set_kernel_variants) and the tuning
   // overrides of the bf16 patch kernel's N tile (0: automatic).
   int vflags, patch_nt;
+  // Split-K (conv_winot5 on grids smaller than the chip): n_split > 1 blocks per output tile, each
+  // over a contiguous range of input-channel chunks, write their partial sums to part[split] (fp32,
+  // [n_split][M][Cout]); a second pass adds them in split order with bias, residual and ReLU.
+  float* part;
+  int n_split;
 };
 
 // Decoder tap: low-resolution projection P_i = (s1 * W_i) . f_i, channels-last with 64 channels.
@@ -89,6 +94,13 @@ bool winot_supported(const ConvParams& p);
 hipError_t launch_winot(const ConvParams& p, hipStream_t s);
 // launch_winot would run conv_winot5, the variant that also reads 8-channel-blocked input (x_c8).
 bool winot_c8_ok(const ConvParams& p);
+// Split-K: y = [relu](sum of p.part[0 .. n_split) in split order + bias + res), fp32 channels-last.
+hipError_t launch_split_sum(const ConvParams& p, hipStream_t s);
+// Split-K factor for launch_conv's conv_dma with M tile mt (1: no split; per-clip shape only).
+int dma_split_for(const ConvParams& p, int mt);
+// Split-K factor (ConvParams::n_split) for launch_winot (1: no split; per-clip shape only); the
+// caller provides ConvParams::part with n_split * M * Cout floats.
+int winot_split_for(const ConvParams& p);
 // U[cin_p/8][6][cout_p/64][64][8] from folded weights w[cout][cin][3] (double).
 void winot_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 // Patch-staged bf16 implicit GEMM for stride-1 1x3x3 and 3x1x1 convs (conv_patch.hip); p.w = conv_dma's

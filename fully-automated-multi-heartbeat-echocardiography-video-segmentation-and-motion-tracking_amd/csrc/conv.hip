@@ -80,6 +80,22 @@ __device__ inline void epilogue(const ConvParams& p, const f32x4 (&acc)[MT][NT],
   }
 }
 
+// Split-K partial sums: acc as is (no bias, residual or ReLU), fp32 channels-last [M][Cout].
+template <int MT, int NT>
+__device__ inline void partial_store(const ConvParams& p, const f32x4 (&acc)[MT][NT], float* part, int m_base, int n0,
+                                     int q, int l16) {
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = m_base + i * 16 + l16;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = n0 + j * 16 + 4 * q;
+      if (n < p.Cout) *reinterpret_cast<f32x4*>(part + (size_t)m * p.Cout + n) = acc[i][j];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // LDS-DMA implicit GEMM. T = float (K step 16) or __bf16 (K step 32). 4 waves along M (BM = 64*MT),
 // BN = 16*NT, S-stage ring. Requires Cin (and Cin2) % (K step) == 0.
@@ -109,7 +125,11 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
   const T* w = reinterpret_cast<const T*>(p.w);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int n_split = p.n_split > 1 ? p.n_split : 1;
+  int tile = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int n_tb = gridDim.x / n_split;  // output tiles
+  const int split = tile / n_tb;
+  tile -= split * n_tb;
   const int tq = fdiv(tile, dv.nt);
   const int m0 = tq * BM, n0 = (tile - tq * n_tiles) * BN;
   const int q = lane >> 4, l16 = lane & 15;
@@ -144,11 +164,30 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
   const int khw = p.KH * p.KW;
   const int kmain = p.KT * khw * p.Cin;  // K columns from x; the rest (1x1 dual input) from x2
 
-  // K-step cursor (issue() is called for k_step = 0, 1, 2, ... in order): channel offset c0 inside
+  // split-K (p.n_split > 1): this block sums K steps [kb, ke) of its tile
+  const int nk_all = p.Kp / BKE;
+  const int kb = split * nk_all / n_split, ke = (split + 1) * nk_all / n_split;
+
+  // K-step cursor (issue() is called for k_step = kb, kb + 1, ... in order): channel offset c0 inside
   // tap (kt, kh, kw) of input x, then of x2 -- advanced incrementally, where the per-step scalar
-  // divisions of the closed form cost ~3 SALU instructions per MFMA (PMC, layer2 SP1)
+  // divisions of the closed form cost ~3 SALU instructions per MFMA (PMC, layer2 SP1); the closed
+  // form once for the start
   int c_c0 = 0, c_kt = 0, c_kh = 0, c_kw = 0, c_tap_pix = 0;
   bool c_second = kmain == 0;
+  if (kb > 0) {
+    const int e0 = kb * BKE;
+    if (e0 >= kmain) {
+      c_second = true;
+      c_c0 = e0 - kmain;
+    } else {
+      const int tap = e0 / p.Cin;
+      c_c0 = e0 - tap * p.Cin;
+      c_kw = tap % p.KW;
+      c_kh = (tap / p.KW) % p.KH;
+      c_kt = tap / khw;
+      c_tap_pix = (c_kt * p.Hi + c_kh) * p.Wi + c_kw;
+    }
+  }
   auto issue = [&](int k_step, int slot) {
     const int k0 = k_step * BKE;
     const bool second = c_second;
@@ -195,10 +234,10 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.Kp / BKE;
+  const int nk = ke - kb;
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
-    if (s < nk) issue(s, s);
+    if (s < nk) issue(kb + s, s);
 
   const int pq = q ^ G[l16 >> 2];  // physical slot of this lane's fragment reads
   const int a_off = (wid * 16 * MT + l16) * 64 + pq * 16;
@@ -216,7 +255,7 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (k + S - 1 < nk) issue(k + S - 1, (k + S - 1) % S);
+    if (k + S - 1 < nk) issue(kb + k + S - 1, (k + S - 1) % S);
     const char* st = smem + (k % S) * STAGE;
     if constexpr (sizeof(T) == 4) {
       f32x4 a[MT], b[NT];
@@ -243,7 +282,10 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
         for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
     }
   }
-  epilogue<MT, NT>(p, acc, m0 + wid * 16 * MT, n0, q, l16);
+  if (n_split > 1)
+    partial_store<MT, NT>(p, acc, p.part + (size_t)split * p.M * p.Cout, m0 + wid * 16 * MT, n0, q, l16);
+  else
+    epilogue<MT, NT>(p, acc, m0 + wid * 16 * MT, n0, q, l16);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -467,7 +509,9 @@ hipError_t launch_dma(const ConvParams& p, hipStream_t s) {
   constexpr int BM = 64 * MT, BN = 16 * NT;
   const int mt = (p.M + BM - 1) / BM, nt = (p.Cout + BN - 1) / BN;
   const DmaDivs dv{fast_div(p.Wo), fast_div(p.Ho), fast_div(p.To), fast_div(nt)};
-  hipLaunchKernelGGL((conv_dma<T, MT, NT, S>), dim3(mt * nt), dim3(256), 0, s, p, nt, dv);
+  const int n_split = p.n_split > 1 ? p.n_split : 1;
+  hipLaunchKernelGGL((conv_dma<T, MT, NT, S>), dim3(mt * nt * n_split), dim3(256), 0, s, p, nt, dv);
+  if (n_split > 1) return launch_split_sum(p, s);
   return hipGetLastError();
 }
 
@@ -524,6 +568,42 @@ void conv_pick_tile(int M, int cout_p, int force_nt, int* mt_out, int* bn_out) {
   (void)M;
   *mt_out = 2;
   *bn_out = 16 * nt;
+}
+
+// y = [relu](sum over splits, in split order, of part[split] + bias + res): fp32 channels-last,
+// 4 floats per lane (Cout % 4 == 0)
+__global__ __launch_bounds__(256) void split_sum_kernel(const float* __restrict__ part, int n_split, long n4, int co4,
+                                                        const float* __restrict__ bias, const float* res, int relu,
+                                                        float* y) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const f32x4* pp = reinterpret_cast<const f32x4*>(part);
+  f32x4 v = pp[i];
+  for (int k = 1; k < n_split; ++k) v += pp[(long)k * n4 + i];
+  if (bias) v += reinterpret_cast<const f32x4*>(bias)[i % co4];
+  if (res) v += reinterpret_cast<const f32x4*>(res)[i];
+  if (relu)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.f);
+  reinterpret_cast<f32x4*>(y)[i] = v;
+}
+
+hipError_t launch_split_sum(const ConvParams& p, hipStream_t s) {
+  if (p.in_bf16 || p.out_bf16 || p.y_c8 || p.Cout % 4 || !p.part) return hipErrorInvalidValue;
+  const long n4 = (long)p.M * p.Cout / 4;
+  hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, p.part, p.n_split, n4,
+                     p.Cout / 4, p.bias, (const float*)p.res, p.relu, (float*)p.y);
+  return hipGetLastError();
+}
+
+// Split-K factor for conv_dma (fp32, channels-last output): as winot_split_for -- maps of <= 256
+// output voxels per clip (layer4's temporal stride-2 conv at 112x112 clips: 184 tiles for 30 clips)
+// split K into 4 ranges of >= 16 steps; the factor depends on the per-clip shape only, never on the
+// batch size.
+int dma_split_for(const ConvParams& p, int mt) {
+  if (p.in_bf16 || p.out_bf16 || p.y_c8 || p.stem || mt != 2 || (p.vflags & CLASFV_VARIANT_NO_SPLIT_K)) return 1;
+  if ((long)p.To * p.Ho * p.Wo > 256 || p.Kp / 16 < 4 * 16) return 1;
+  return 4;
 }
 
 hipError_t launch_conv(const ConvParams& p, int mt, int bn, hipStream_t s) {

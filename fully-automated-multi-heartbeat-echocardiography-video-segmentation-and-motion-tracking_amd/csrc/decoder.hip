@@ -143,14 +143,18 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
   for (int r = 0; r < 4; ++r) hb[r] = 4 * q + r < 6 ? p.bh[4 * q + r] : 0.f;
   const size_t HW = (size_t)p.H * p.W;
   const size_t TH = (size_t)p.T * HW;
+  f32x4 outs[2] = {hb, hb};  // head bias (rows 4q + r < 6) in the accumulator
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        outs[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[mt][nt][r], outs[mt], 0, 0, 0);
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     const int hr = h0 + 2 * wid + mt;
-    f32x4 out = hb;  // head bias (rows 4q + r < 6) in the accumulator
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) out = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[mt][nt][r], out, 0, 0, 0);
+    const f32x4 out = outs[mt];
     if (q < 2) {
       const size_t pix = (size_t)t * HW + (size_t)hr * p.W + (w0 + l16);
 #pragma unroll
@@ -172,8 +176,11 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
 // BF = 1 (BASELINE config[4]): comb_2 on v_mfma_f32_16x16x32_bf16 with split (hi + lo) bf16 h1 and W2
 // (one 32-deep K block = the 8 channels 16c + 4q + j, c in {2kb, 2kb+1}, that lane group q already
 // holds, so both operands keep the fp32 path's register layout), fp32 accumulation; fp32 heads.
-template <int BF>
+// MODE: 0 = fp32, 1 = bf16 comb_2; timing knock-outs for tools/convbench.hip (CLASFV_KNOCKOUTS builds
+// only; wrong results): 2 = no comb_2 / head MFMAs, 3 = no interpolation.
+template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void decoder_kernel(DecParams p) {
+  constexpr int BF = MODE == 1;
   extern __shared__ __align__(16) float smem[];
   float* stage = smem;  // STAGE_FLOATS
 
@@ -279,6 +286,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
   const int hr = h0 + 2 * wid;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
+    if constexpr (MODE == 3) {  // knock-out: one LDS read per channel group instead of the interpolation
+#pragma unroll
+      for (int c = 0; c < 4; ++c) h1[0][c] += *reinterpret_cast<const f32x4*>(stage + kPixOff[i] * PIX + 4 * q + 16 * c + l16 * PIX);
+      continue;
+    }
     const DecTap& tp = p.tap[i];
     const Win& w = win[i];
     int x0, x1, ya0, ya1, yb0, yb1;
@@ -344,18 +356,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
         wn[c] = *reinterpret_cast<const f32x4*>(p.w2 + ((nt + 1) * 16 + l16) * 64 + 16 * c + 4 * q);
     }
     const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
+    acc[0][nt] = bb;  // the bias rides in the accumulator
+    acc[1][nt] = bb;
+    if constexpr (MODE == 2) {  // knock-out: no MFMA
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      acc[mt][nt] = bb;  // the bias rides in the accumulator
+      for (int mt = 0; mt < 2; ++mt) acc[mt][nt] += wa[nt] * h1[mt][nt];
+    } else {
+      // one accumulator chain at a time (alternating the two rows' chains measured the same: 1.608 vs
+      // 1.598 ms, profiles/r03d_decoder_variants.txt)
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
+      for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[c][j], h1[mt][c][j], acc[mt][nt], 0, 0, 0);
-      // acc[mt][nt][r] = h2^T[ch = 16nt + 4q + r][voxel l16]
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[c][j], h1[mt][c][j], acc[mt][nt], 0, 0, 0);
+    }
+    // acc[mt][nt][r] = h2^T[ch = 16nt + 4q + r][voxel l16]
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[mt][nt][r] = fmaxf(acc[mt][nt][r], 0.f);
-    }
 #pragma unroll
     for (int c = 0; c < 4; ++c) wa[c] = wn[c];
   }
@@ -369,14 +390,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
   f32x4 hb;
 #pragma unroll
   for (int r = 0; r < 4; ++r) hb[r] = 4 * q + r < 6 ? p.bh[4 * q + r] : 0.f;
+  f32x4 outs[2] = {hb, hb};  // head bias (rows 4q + r < 6) in the accumulator
+  if constexpr (MODE == 2) {
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int hr = h0 + 2 * wid + mt;
-    f32x4 out = hb;  // head bias (rows 4q + r < 6) in the accumulator
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) outs[mt] += wh[nt] * acc[mt][nt];
+  } else {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[mt][nt][r], out, 0, 0, 0);
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          outs[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[mt][nt][r], outs[mt], 0, 0, 0);
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int hr = h0 + 2 * wid + mt;
+    const f32x4 out = outs[mt];
     // 5. out[r] = head (4q + r) at voxel (hr, w0 + l16)
     if (q < 2) {
       const size_t pix = (size_t)t * HW + (size_t)hr * p.W + (w0 + l16);
@@ -396,34 +428,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
 
 }  // namespace
 
-static hipError_t launch_dec(const DecParams& p, hipStream_t s) {
+static hipError_t launch_dec(const DecParams& p, hipStream_t s, int mode) {
   if (p.tap[0].T != p.T) return hipErrorInvalidValue;  // tap 0 is staged as a single frame
   for (int i = 0; i < 4; ++i)  // the staging loads use 32-bit element offsets
     if ((size_t)p.N * p.tap[i].T * p.tap[i].H * p.tap[i].W * 64 >= ((size_t)1 << 31)) return hipErrorInvalidValue;
   const size_t nb = (size_t)(p.H / TILE_H) * (p.W / TILE_W) * p.T * p.N;
   if (nb >= ((size_t)1 << 31)) return hipErrorInvalidValue;
-  const size_t lds = (size_t)STAGE_FLOATS * 4;
-  static bool attr_set = false;
-  if (!attr_set) {
-    for (const void* k : {(const void*)decoder_kernel<0>, (const void*)decoder_kernel<1>}) {
-      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return e;
-    }
-    attr_set = true;
-  }
-  if (p.bf16)
-    hipLaunchKernelGGL(decoder_kernel<1>, dim3((unsigned)nb), dim3(256), lds, s, p);
-  else
-    hipLaunchKernelGGL(decoder_kernel<0>, dim3((unsigned)nb), dim3(256), lds, s, p);
+  constexpr size_t lds = (size_t)STAGE_FLOATS * 4;
+  static_assert(lds <= 64 * 1024, "default dynamic LDS limit");
+  void (*k)(DecParams) = mode == 1 ? decoder_kernel<1> : decoder_kernel<0>;
+#ifdef CLASFV_KNOCKOUTS
+  if (mode == 2) k = decoder_kernel<2>;
+  if (mode == 3) k = decoder_kernel<3>;
+#endif
+  hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 
-hipError_t launch_decoder(const DecParams& p, hipStream_t s) { return launch_dec(p, s); }
+hipError_t launch_decoder(const DecParams& p, hipStream_t s) { return launch_dec(p, s, p.bf16 ? 1 : 0); }
 
 #ifdef CLASFV_KNOCKOUTS
-// tools/convbench.hip
+// tools/convbench.hip: ko 0 = product; 2, 3 = decoder_kernel's knock-out modes
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko) {
-  (void)ko;
-  return launch_dec(p, s);
+  return launch_dec(p, s, ko == 2 || ko == 3 ? ko : (p.bf16 ? 1 : 0));
 }
 #endif

@@ -110,6 +110,7 @@ int env_variants() {
   if (on("CLASFV_NO_PATCH_BF16")) f |= CLASFV_VARIANT_NO_PATCH_BF16;
   if (on("CLASFV_NO_DECODER_BF16")) f |= CLASFV_VARIANT_NO_DECODER_BF16;
   if (ts1 && ts1[0] == '0') f |= CLASFV_VARIANT_WINOT_NO_TS1;
+  if (on("CLASFV_NO_SPLIT_K")) f |= CLASFV_VARIANT_NO_SPLIT_K;
   return f;
 }
 
@@ -392,7 +393,7 @@ bool c8_pair(const Conv& a, const Conv& b, const Shape5& in, const Tuning& tu) {
 
 int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
              hipStream_t s, const void* zero_block, const void* x2, const char** kname, const Tuning& tu, int x_c8 = 0,
-             int y_c8 = 0) {
+             int y_c8 = 0, void* scratch = nullptr, size_t scratch_bytes = 0) {
   if (in.c != c.cin_p) return fail(CLASFV_EINVAL, "internal: channel mismatch");
   ConvParams p = conv_params(c, in, out);
   p.vflags = tu.vflags;
@@ -421,6 +422,12 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
     HIP_TRY(launch_stem_bf16(p, s));
   } else if (!strcmp(k, "conv_winot")) {
     p.w = c.dwinot;
+    // split-K on the smallest maps (per-clip shape rule), partial sums in the caller's scratch
+    const int S = winot_split_for(p);
+    if (S > 1 && scratch && (size_t)S * p.M * p.Cout * sizeof(float) <= scratch_bytes) {
+      p.part = reinterpret_cast<float*>(scratch);
+      p.n_split = S;
+    }
     HIP_TRY(launch_winot(p, s));
   } else if (!strcmp(k, "conv_patch_bf16")) {
     HIP_TRY(launch_patch_bf16(p, s));
@@ -429,6 +436,12 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
     if (!c.stem) {
       conv_pick_tile(p.M, c.cout_p, tu.conv_nt, &mt, &bn);
       if (tu.conv_mt == 4 && p.in_bf16) mt = 4;  // tuning override
+      // split-K on the smallest maps (per-clip shape rule), partial sums in the caller's scratch
+      const int S = dma_split_for(p, mt);
+      if (S > 1 && scratch && (size_t)S * p.M * p.Cout * sizeof(float) <= scratch_bytes) {
+        p.part = reinterpret_cast<float*>(scratch);
+        p.n_split = S;
+      }
     }
     HIP_TRY(launch_conv(p, mt, bn, s));
   }
@@ -722,7 +735,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0xFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~0x1FF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;
@@ -758,10 +771,22 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
     if (e >= 0) h->recs.push_back({name, gflop, xgflop, last_ev, e});
     last_ev = e;
   };
+  // scratch for a temporal conv reading MID: the rest of MID past its input
+  const size_t mid_bytes = L.off[MID + 1] - L.off[MID];
   auto run = [&](const Conv& c, const void* xin, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
                  const void* x2 = nullptr, int x_c8 = 0, int y_c8 = 0) {
     const char* kname = "";
-    int rc_ = run_conv(c, xin, in, y, out, res, relu, s, h->zero, x2, &kname, h->tune, x_c8, y_c8);
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    if (xin == buf(MID)) {
+      const size_t used = ((size_t)in.n * in.t * in.h * in.w * in.c * sizeof(float) + 255) / 256 * 256;
+      if (used < mid_bytes) {
+        scratch = h->arena + L.off[MID] + used;
+        scratch_bytes = mid_bytes - used;
+      }
+    }
+    int rc_ = run_conv(c, xin, in, y, out, res, relu, s, h->zero, x2, &kname, h->tune, x_c8, y_c8, scratch,
+                       scratch_bytes);
     if (!rc_) timed(kname, conv_gflop(c, out), conv_exec_gflop(c, out, kname));
     return rc_;
   };

@@ -275,7 +275,9 @@ struct T5 {
   static_assert(NF * P * 2 % 64 == 0, "whole DMA instructions");
 };
 
-// EPI: epilogue form, bit 0 = residual add, bit 1 = ReLU (compile-time, no per-element selects).
+// EPI: epilogue form, bit 0 = residual add, bit 1 = ReLU (compile-time, no per-element selects);
+// bit 2 = split-K partial: the block sums input-channel chunks [k0, k1) of its split only and stores
+// y = A^T M without bias, residual or ReLU to p.part[split] (launch_split_sum finishes).
 template <int TS, int NT, int EPI>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_winot5(ConvParams p, int n_co,
                                                                                              int n_seg, int n_cols,
@@ -287,13 +289,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, l16 = lane & 15;
-  const int blk = xcd_swizzle_t(blockIdx.x, gridDim.x);
+  constexpr bool SPLIT = (EPI & 4) != 0;
+  int blk = xcd_swizzle_t(blockIdx.x, gridDim.x);
+  const int nb = gridDim.x / (SPLIT ? p.n_split : 1);
+  const int split = SPLIT ? blk / nb : 0;
+  blk -= split * nb;
   const int co_blk = blk % n_co, rest = blk / n_co;
   const int seg = rest % n_seg, cb = rest / n_seg;
   const int col0 = cb * G::P, co0 = co_blk * G::CB;
   const int T = p.To, HW = p.Ho * p.Wo, C = p.Cin, CO = p.Cout;
   const int t_seg = seg * 4 * TS;
   const int nchunk = C >> 3;
+  const int k0 = SPLIT ? split * nchunk / p.n_split : 0;
+  const int k1 = SPLIT ? (split + 1) * nchunk / p.n_split : nchunk;
   // input pixel stride and chunk stride (floats): channels-last, or 8-channel blocks (x_c8)
   const int cs = p.x_c8 ? 8 : C;
   const size_t kstride = p.x_c8 ? (size_t)p.N * T * HW * 8 : 8;
@@ -357,16 +365,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[e][m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  issue(0, 0);
+  issue(k0, 0);
   __builtin_amdgcn_sched_barrier(0);
-  for (int k = 0; k < nchunk; ++k) {
+  for (int k = k0; k < k1; ++k) {
     __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): chunk k's DMAs (own) landed
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();        // everyone's landed; everyone done with the other stage
     __builtin_amdgcn_sched_barrier(0);
-    if (k + 1 < nchunk) issue(k + 1, (k + 1) & 1);
+    if (k + 1 < k1) issue(k + 1, (k + 1 - k0) & 1);
     __builtin_amdgcn_sched_barrier(0);
-    const float* st = reinterpret_cast<const float*>(smem + (k & 1) * G::STAGE);
+    const float* st = reinterpret_cast<const float*>(smem + ((k - k0) & 1) * G::STAGE);
     // frames of tile m: d[4m .. 4m + 5] (in time), or d[6m .. 6m + 5] (COLS: the m-th column group)
     constexpr int ND = COLS ? 12 : 10, MS = COLS ? 6 : 4;
     f32x2 d[ND];
@@ -413,7 +421,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
   // epilogue: y = A^T M in registers, 16-B bias / residual loads and stores
   const float* res = reinterpret_cast<const float*>(p.res);
-  float* yout = reinterpret_cast<float*>(p.y);
+  float* yout = SPLIT ? p.part + (size_t)split * ((size_t)p.N * T * HW * CO) : reinterpret_cast<float*>(p.y);
   const size_t fstride = (size_t)HW * CO;
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
@@ -426,7 +434,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int nt = 0; nt < NT; ++nt) {
       const int co = co0 + 16 * nt + 4 * q;
       const size_t o = ((size_t)(n * T + t0) * HW + pix) * CO + co;
-      const f32x4 bv = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 bv = (p.bias && !SPLIT) ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
       f32x4 rv[4];
 #pragma unroll
       for (int a2 = 0; a2 < 4; ++a2)
@@ -442,7 +450,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if (ok) {
 #pragma unroll
         for (int a2 = 0; a2 < 4; ++a2) {
-          f32x4 vv = yv[a2] + bv;
+          f32x4 vv = SPLIT ? yv[a2] : yv[a2] + bv;
           if constexpr (EPI & 1) vv += rv[a2];
           if constexpr (EPI & 2) {
 #pragma unroll
@@ -468,7 +476,7 @@ hipError_t winot5_launch_e(const ConvParams& p, hipStream_t s) {
   const int n_cols = p.N * p.Hi * p.Wi;
   const int n_seg = (p.Ti / 4) / TS;
   const int n_co = p.Cout / G::CB;
-  const int nb = ((n_cols + G::P - 1) / G::P) * n_seg * n_co;
+  const int nb = ((n_cols + G::P - 1) / G::P) * n_seg * n_co * ((EPI & 4) ? p.n_split : 1);
   hipLaunchKernelGGL((conv_winot5<TS, NT, EPI>), dim3(nb), dim3(256), G::LDS, s, p, n_co, n_seg, n_cols,
                      fast_div(p.Hi * p.Wi));
   return hipGetLastError();
@@ -476,6 +484,11 @@ hipError_t winot5_launch_e(const ConvParams& p, hipStream_t s) {
 
 template <int TS, int NT>
 hipError_t winot5_launch(const ConvParams& p, hipStream_t s) {
+  if (p.n_split > 1) {
+    hipError_t e = winot5_launch_e<TS, NT, 4>(p, s);  // bias, residual and ReLU in the sum pass
+    if (e != hipSuccess) return e;
+    return launch_split_sum(p, s);
+  }
   switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
     case 2: return winot5_launch_e<TS, NT, 2>(p, s);  // TP1 / stem T: BN + ReLU
     case 3: return winot5_launch_e<TS, NT, 3>(p, s);  // TP2: BN + residual + ReLU
@@ -485,11 +498,19 @@ hipError_t winot5_launch(const ConvParams& p, hipStream_t s) {
 }
 
 // 64 channels per wave (NT = 4); 32 when that leaves fewer than two blocks per CU (layer3 maps).
-hipError_t winot5_dispatch(const ConvParams& p, hipStream_t s, int force_nt = 0) {
+int winot5_nt(const ConvParams& p, long* blocks) {
   const int tt = p.Ti / 4;
   const int ts = tt % 4 == 0 ? 4 : tt % 2 == 0 ? 2 : 1;
   const long blocks64 = (long)((p.N * p.Hi * p.Wi + 16 * 8 / ts - 1) / (16 * 8 / ts)) * (tt / ts) * (p.Cout / 64);
-  const int nt = force_nt ? force_nt : (blocks64 >= 512 ? 4 : 2);
+  const int nt = blocks64 >= 512 ? 4 : 2;
+  if (blocks) *blocks = blocks64 * (4 / nt);
+  return nt;
+}
+
+hipError_t winot5_dispatch(const ConvParams& p, hipStream_t s, int force_nt = 0) {
+  const int tt = p.Ti / 4;
+  const int ts = tt % 4 == 0 ? 4 : tt % 2 == 0 ? 2 : 1;
+  const int nt = force_nt ? force_nt : winot5_nt(p, nullptr);
   if (ts == 4) return nt == 4 ? winot5_launch<4, 4>(p, s) : winot5_launch<4, 2>(p, s);
   if (ts == 1) return nt == 4 ? winot5_launch<1, 4>(p, s) : winot5_launch<1, 2>(p, s);
   return nt == 4 ? winot5_launch<2, 4>(p, s) : winot5_launch<2, 2>(p, s);
@@ -511,6 +532,17 @@ static bool winot5_ok(const ConvParams& p) {
   if (winot_c8_ok(p)) return true;
   return !(p.vflags & (CLASFV_VARIANT_WINOT_NO_TS1 | CLASFV_VARIANT_WINOT_REFERENCE)) && !p.x_c8 && winot_supported(p) &&
          winot5_fits(p);
+}
+
+// Split-K factor for conv_winot5 (ConvParams::n_split). Layer4 at 112x112 clips (4 x 7 x 7 output
+// voxels per clip) runs 192 blocks for 30 clips: one per CU on three quarters of the chip, one wave per
+// SIMD. Maps of <= 256 output voxels per clip split their input channels into 4 ranges of >= 8 chunks
+// (768 blocks for 30 clips). The factor depends on the per-clip shape only, never on the batch size,
+// so a clip's result does not depend on the clips batched with it.
+int winot_split_for(const ConvParams& p) {
+  if (!winot5_ok(p) || p.x_c8 || (p.vflags & CLASFV_VARIANT_NO_SPLIT_K)) return 1;
+  if ((long)p.To * p.Ho * p.Wo > 256 || p.Cin / 8 < 4 * 8) return 1;
+  return 4;
 }
 
 bool winot_supported(const ConvParams& p) {
@@ -557,6 +589,11 @@ hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 500: return p.x_c8 && !winot_c8_ok(p) ? hipErrorInvalidValue : winot5_dispatch(p, s);
     case 502: return winot5_dispatch(p, s, 2);
     case 504: return winot5_dispatch(p, s, 4);
+  }
+  if (ko >= 600 && ko < 700 && p.part && !p.x_c8) {  // split-K: 6 NT S (p.part holds 8 partials)
+    ConvParams q = p;
+    q.n_split = ko % 10;
+    return q.n_split > 8 ? hipErrorInvalidValue : winot5_dispatch(q, s, (ko / 10) % 10);
   }
   return hipErrorInvalidValue;
 }

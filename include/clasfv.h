@@ -56,8 +56,9 @@ enum { CLASFV_FUSE_MAJORITY = 0, CLASFV_FUSE_SIMPLE = 1, CLASFV_FUSE_STAPLE = 2,
 enum { CLASFV_DTYPE_FP32 = 0, CLASFV_DTYPE_BF16 = 1 };
 
 /* Kernel-variant switches (A/B testing against the kernels each product kernel replaced; every
- * variant computes the same function). Read once, at clasfv_create, from the environment variable
- * named in the comment (set = on), or set with clasfv_set_kernel_variants. */
+ * variant computes the same function -- NO_SPLIT_K the same sums in another fp32 summation order).
+ * Read once, at clasfv_create, from the environment variable named in the comment (set = on), or set
+ * with clasfv_set_kernel_variants. */
 enum {
   CLASFV_VARIANT_NO_WINOGRAD = 1,      /* CLASFV_WINOGRAD=0: fp32 stride-1 convs on the direct implicit GEMM */
   CLASFV_VARIANT_NO_WINO_PATCH = 2,    /* CLASFV_NO_WINO_PATCH: conv_wino instead of conv_wino_q */
@@ -66,7 +67,8 @@ enum {
   CLASFV_VARIANT_NO_STEM_BF16 = 16,    /* CLASFV_NO_STEM_BF16: bf16 engines run the fp32 stem */
   CLASFV_VARIANT_NO_PATCH_BF16 = 32,   /* CLASFV_NO_PATCH_BF16: bf16 stride-1 convs on conv_dma */
   CLASFV_VARIANT_NO_DECODER_BF16 = 64, /* CLASFV_NO_DECODER_BF16: bf16 engines run the fp32 decoder */
-  CLASFV_VARIANT_WINOT_NO_TS1 = 128    /* CLASFV_WINOT_TS1=0: T % 8 != 0 temporal convs on conv_winot */
+  CLASFV_VARIANT_WINOT_NO_TS1 = 128,   /* CLASFV_WINOT_TS1=0: T % 8 != 0 temporal convs on conv_winot */
+  CLASFV_VARIANT_NO_SPLIT_K = 256      /* CLASFV_NO_SPLIT_K: conv_winot5 grids smaller than the chip unsplit */
 };
 
 typedef struct clasfv_engine* clasfv_t;

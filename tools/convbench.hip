@@ -115,6 +115,9 @@ int main(int argc, char** argv) {
   p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
   p.res = getenv("CB_NORES") ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
   CK(hipMalloc(&p.y, ny * 4));
+  for (int ko : kos)
+    if (((winot && ko >= 600 && ko < 700) || (!wino && !winot && ko >= 700 && ko < 709)) && !p.part)
+      CK(hipMalloc((void**)&p.part, 8 * ny * 4));  // split-K partials
   void* z;
   CK(hipMalloc(&z, 256));
   CK(hipMemset(z, 0, 256));
@@ -137,7 +140,9 @@ int main(int argc, char** argv) {
       int mt, bn;
       conv_pick_tile(p.M, Cout, getenv("CB_NT") ? atoi(getenv("CB_NT")) : 0, &mt, &bn);
       if (getenv("CB_MT")) mt = atoi(getenv("CB_MT"));
-      CK(launch_conv(p, mt, bn, s));
+      ConvParams q = p;
+      if (ko >= 700 && ko < 709) q.n_split = ko - 700;  // conv_dma split-K into ko - 700 K ranges
+      CK(launch_conv(q, mt, bn, s));
     }
   };
   // warm every variant up (clocks settle), then interleave 3 timed rounds and keep each one's best
