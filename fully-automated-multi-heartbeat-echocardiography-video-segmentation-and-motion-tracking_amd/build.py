@@ -13,7 +13,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 INCLUDE = os.path.join(REPO_DIR, "include")
 LIB_PATH = os.path.join(PKG_DIR, "libclasfv.so")
-SOURCES = ["engine.hip", "conv.hip", "conv_patch.hip", "winograd.hip", "winograd2.hip", "winograd_t.hip",
+SOURCES = ["engine.hip", "conv.hip", "conv_patch.hip", "winograd.hip", "winograd2.hip", "winograd4.hip", "winograd_t.hip",
            "decoder.hip", "plumbing.hip"]
 HEADERS = ["common.h", "plumbing.h"]
 ARCH = os.environ.get("CLASFV_OFFLOAD_ARCH", "gfx950")

@@ -89,6 +89,14 @@ void wino_transform_weights(const double* w, int cout, int cin, int cout_p, int 
 // Patch-tiled Winograd F(2x2,3x3) for Ho, Wo % 4 == 0 (winograd2.hip); p.w = conv_wino's U.
 bool winoq_supported(const ConvParams& p);
 hipError_t launch_winoq(const ConvParams& p, hipStream_t s);
+// Fused Winograd F(4x4,3x3) for stride-1 1x3x3 fp32 convs with Ho, Wo % 4 == 0, no residual
+// (winograd4.hip); p.w = wino4_transform_weights' layout.
+bool wino4_supported(const ConvParams& p);
+hipError_t launch_wino4(const ConvParams& p, hipStream_t s);
+// MFMA work (GFLOP) one conv_wino4 launch executes (16 MFMA rows per tile group, padding included).
+double wino4_exec_gflop(const ConvParams& p);
+// U[cout_p/48][cin_p/8][6][3][3][64][4] from folded weights w[cout][cin][3][3] (double).
+void wino4_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 // Fused Winograd F(4,3)-in-time path for stride-1 3x1x1 fp32 convs; p.w = transformed weights.
 bool winot_supported(const ConvParams& p);
 hipError_t launch_winot(const ConvParams& p, hipStream_t s);

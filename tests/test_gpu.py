@@ -544,19 +544,41 @@ def test_winograd_path_matches_direct_conv(model, shape):
 def test_kernel_variants_bitexact(model, shape):
     """The patch-tiled spatial Winograd kernel (conv_wino_q) and the rolling-halo temporal one
     (conv_winot5) compute the same products in the same accumulation order as conv_wino / conv_winot:
-    the forward must be bit-identical with them switched off. Split-K (conv_winot5 / conv_dma on maps of
-    <= 256 voxels per clip: layer4) sums the same products in another order: within 5e-5."""
+    the forward must be bit-identical with them switched off (F(2x2,3x3) everywhere: variant
+    no_wino4). Split-K (conv_winot5 / conv_dma on maps of <= 256 voxels per clip: layer4) sums the
+    same products in another order: within 5e-5."""
     rng = np.random.default_rng(23)
     x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    model.set_kernel_variants("no_wino4")
     s_split, m_split = model(x)
-    model.set_kernel_variants("no_split_k")
+    model.set_kernel_variants("no_wino4", "no_split_k")
     s_new, m_new = model(x)
-    model.set_kernel_variants("no_wino_patch", "winot_reference", "no_split_k")
+    model.set_kernel_variants("no_wino4", "no_wino_patch", "winot_reference", "no_split_k")
     s_old, m_old = model(x)
     model.set_kernel_variants()
     assert torch.equal(s_new, s_old) and torch.equal(m_new, m_old)
     # summation order only: a few ulps of the layer4 sums, grown through the decoder (logits ~5)
     assert (s_split - s_new).abs().max().item() <= 5e-5 and (m_split - m_new).abs().max().item() <= 5e-6
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (3, 3, 24, 32, 32), (2, 3, 16, 64, 48)])
+def test_wino4_matches_wino2(model, shape):
+    """conv_wino4 (Winograd F(4x4,3x3), the default for the layer1/layer2 spatial convs) against
+    conv_wino_q / conv_wino (F(2x2,3x3), variant no_wino4): different fp32 rounding of the same
+    convolution, within the forward bar; the mask labels agree except where |l1 - l0| is at that
+    rounding level. Shapes cover 14-, 12- and 16-tile groups and groups spanning two frames."""
+    rng = np.random.default_rng(41)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    s4, m4 = model(x)
+    model.set_kernel_variants("no_wino4")
+    s2, m2 = model(x)
+    model.set_kernel_variants()
+    assert not torch.equal(s4, s2)  # the F(4x4) kernel really ran
+    np.testing.assert_allclose(s4.cpu().numpy(), s2.cpu().numpy(), rtol=0, atol=SEG_ATOL)
+    np.testing.assert_allclose(m4.cpu().numpy(), m2.cpu().numpy(), rtol=0, atol=MOT_ATOL)
+    d = (s4[:, 1] - s4[:, 0]).cpu().numpy()
+    flips = ((s4[:, 1] > s4[:, 0]) != (s2[:, 1] > s2[:, 0])).cpu().numpy()
+    assert np.all(np.abs(d[flips]) <= 2 * SEG_ATOL)
 
 
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (1, 3, 8, 32, 48)])

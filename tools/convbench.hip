@@ -86,7 +86,8 @@ int main(int argc, char** argv) {
   if (kos.empty()) kos.push_back(0);
   const bool winoqp = !strcmp(kind, "winoqp");  // conv_wino_q knock-out probes (tools/winoq_probe.hip)
   const bool winoq = !strcmp(kind, "winoq") || winoqp, winor = !strcmp(kind, "winor");
-  const bool wino = !strcmp(kind, "wino") || winoq || winor, winot = !strcmp(kind, "winot");
+  const bool wino4 = !strcmp(kind, "wino4");  // conv_wino4 (F(4x4,3x3); no residual)
+  const bool wino = !strcmp(kind, "wino") || winoq || winor || wino4, winot = !strcmp(kind, "winot");
   const bool spp = !strcmp(kind, "spp"), tpp = !strcmp(kind, "tpp");  // bf16 patch-staged (conv_patch.hip)
   const bool sp = wino || spp || !strcmp(kind, "sp"), tp = winot || tpp || !strcmp(kind, "tp");
   ConvParams p;
@@ -110,10 +111,10 @@ int main(int argc, char** argv) {
   p.relu = 1;
   const size_t nx = (size_t)N * T * H * W * Cin, ny = (size_t)p.M * Cout;
   p.x = bf ? to_bf16_dev(nx, 0.f, 1.f, 1) : dev_random(nx, 0.f, 1.f, 1);
-  const size_t nw = winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
+  const size_t nw = wino4 ? (size_t)36 * Cin * Cout : winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
   p.w = bf ? to_bf16_dev(nw, -0.05f, 0.05f, 2) : dev_random(nw, -0.05f, 0.05f, 2);
   p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
-  p.res = getenv("CB_NORES") ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
+  p.res = (getenv("CB_NORES") || wino4) ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
   CK(hipMalloc(&p.y, ny * 4));
   for (int ko : kos)
     if (((winot && ko >= 600 && ko < 700) || (!wino && !winot && ko >= 700 && ko < 709)) && !p.part)
@@ -129,7 +130,8 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   auto launch = [&](int ko) {
-    if (winor) CK(launch_winor_ko(p, s, ko));
+    if (wino4) CK(launch_wino4(p, s));
+    else if (winor) CK(launch_winor_ko(p, s, ko));
     else if (winoqp) CK(launch_winoq_probe(p, s, ko));
     else if (winoq) CK(launch_winoq_ko(p, s, ko));
     else if (wino) CK(launch_wino_ko(p, s, ko));
