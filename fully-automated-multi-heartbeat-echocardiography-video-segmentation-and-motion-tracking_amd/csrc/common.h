@@ -89,8 +89,8 @@ void wino_transform_weights(const double* w, int cout, int cin, int cout_p, int 
 // Patch-tiled Winograd F(2x2,3x3) for Ho, Wo % 4 == 0 (winograd2.hip); p.w = conv_wino's U.
 bool winoq_supported(const ConvParams& p);
 hipError_t launch_winoq(const ConvParams& p, hipStream_t s);
-// Fused Winograd F(4x4,3x3) for stride-1 1x3x3 fp32 convs with Ho, Wo % 4 == 0, no residual
-// (winograd4.hip); p.w = wino4_transform_weights' layout.
+// Fused Winograd F(4x4,3x3) for stride-1 1x3x3 fp32 convs without residual (winograd4.hip; partial
+// 4x4 tiles at the edges of maps with Ho, Wo % 4 != 0); p.w = wino4_transform_weights' layout.
 bool wino4_supported(const ConvParams& p);
 hipError_t launch_wino4(const ConvParams& p, hipStream_t s);
 // MFMA work (GFLOP) one conv_wino4 launch executes (16 MFMA rows per tile group, padding included).

@@ -1,6 +1,6 @@
-// Fused Winograd F(4x4, 3x3) for the stride-1 1x3x3 fp32 convs on maps with H, W % 4 == 0 (R(2+1)D-18
-// layer1 and layer2 spatial halves at 112x112 clips: 56x56 and 28x28 maps; torchvision Conv2Plus1D's
-// first conv, called through src/model/R2plus1D_18_MotionNet.py:31-37).
+// Fused Winograd F(4x4, 3x3) for the stride-1 1x3x3 fp32 convs (R(2+1)D-18 Conv2Plus1D spatial halves:
+// 56x56, 28x28, 14x14 and 7x7 maps at 112x112 clips -- the last two with partial edge tiles;
+// torchvision Conv2Plus1D's first conv, called through src/model/R2plus1D_18_MotionNet.py:31-37).
 //
 // Arithmetic: Y = A^T [ sum_ci (G g G^T) (.) (B^T d B) ] A with Lavin's F(4,3) matrices (points 0, +-1,
 // +-2): 36 Winograd-domain products per 4x4 outputs and channel pair instead of conv_wino_q's 64 (F(2x2,
@@ -28,9 +28,9 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int W4_WAVES = 6;
 constexpr int W4_THREADS = 64 * W4_WAVES;
-constexpr int W4_DPW = 3;                            // LDS-DMA instructions per wave per chunk
-constexpr int W4_STAGE = W4_WAVES * W4_DPW * 1024;   // 18 KB raw stage (<= 18 x 64 16-B slots used)
-constexpr int W4_NR = 3;                             // raw ring stages
+constexpr int W4_DPW_MAX = 4;                        // LDS-DMA instructions per wave per chunk (3 or 4)
+constexpr int W4_STAGE = W4_WAVES * W4_DPW_MAX * 1024;  // 24 KB raw stage (<= 24 x 64 16-B slots used)
+constexpr int W4_NR = 3;                                // raw ring stages
 constexpr int W4_ZS = 48 * 17 + 1;                   // epilogue plane [co (stride 17)][tile (16)], odd
 constexpr int W4_LDS = 24 * W4_ZS * 4;               // 78,432 B: Z[i*4+b] planes; ring + sink inside
 static_assert(W4_NR * W4_STAGE + 1024 <= W4_LDS, "ring and sink fit under the epilogue planes");
@@ -54,17 +54,22 @@ struct W4Geo {
   int TR, TC;   // group shape, TR * TC <= 16 tiles
   int TH, TW;   // tiles per frame column / row
   int RP;       // 16-B LDS slots per raw patch row (a pad slot after every 4 pixels: bank spread)
-  int RS;       // slots per channel-half region (6 TR RP); region 1 = input channels 4..7
-  int NI;       // DMA wave-instructions carrying data per stage (<= 18)
+  int SS;       // slots per segment (>= 6 RP: free slots shift the next segment's banks)
+  int RS;       // slots per channel-half region (TR SS); region 1 = input channels 4..7
+  int NI;       // DMA wave-instructions carrying data per stage (<= 6 DPW)
   int n_cob;    // 48-channel output blocks
   int gpr;      // groups per flattened tile row (TW / TC)
-  FastDiv fd_cob, fd_gpr, fd_th, fd_tc, fd_rp;
+  FastDiv fd_cob, fd_gpr, fd_th, fd_tc, fd_rp, fd_ss;
 };
 
 namespace {
 
-// NCH: input-channel chunks (8 channels each; 0 = runtime). C8: 8-channel-blocked output.
-template <int NCH, bool C8, bool RELU>
+// NCH: input-channel chunks (8 channels each; 0 = runtime). C8: 8-channel-blocked output. DPW: DMA
+// instructions per wave per chunk (3: <= 18 per stage; 4: the 8-segment groups of 7x7 maps). KO: timing
+// knock-outs for tools/convbench (0 in the product; results are wrong otherwise): 1 no transform
+// reads / VALU, 2 no U reloads, 4 no epilogue, 8 no DMAs in the chunk loop; 16 (a variant, correct):
+// every window column read from its own address register (no ds_read2_b64 pairing); 32 no chunk barrier.
+template <int NCH, bool C8, bool RELU, int DPW, int KO = 0>
 __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_wino4(ConvParams p,
                                                                                                      W4Geo g) {
   __shared__ __align__(16) char smem[W4_LDS];
@@ -85,19 +90,21 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
   const int NT = g.TR * g.TC;
 
   // ---- LDS-DMA slot table: instruction j of this wave fills slots s = (wid + 6 j) * 64 + lane of a
-  // stage; s < RS: input channels 0..3 of a pixel, else 4..7; within a region slot = row * RP + cs,
-  // row = 6 seg + r (window row r of segment seg), pixel column c = cs - cs / 5 (cs % 5 == 4: pad)
-  unsigned d_off[W4_DPW];  // byte offset of the slot's 16 B in chunk 0, or 0x80000000 (zeros)
+  // stage; s < RS: input channels 0..3 of a pixel, else 4..7; within a region slot = seg * SS + r * RP
+  // + cs (window row r < 6 of segment seg), pixel column c = cs - cs / 5 (cs % 5 == 4: pad)
+  // (array sized by a constant: a template-dependent bound captured by the lambdas below left the
+  // kernels' host stubs undefined under hipcc)
+  unsigned d_off[W4_DPW_MAX];  // byte offset of the slot's 16 B in chunk 0, or 0x80000000 (zeros)
 #pragma unroll
-  for (int j = 0; j < W4_DPW; ++j) {
+  for (int j = 0; j < DPW; ++j) {
     const int ins = wid + W4_WAVES * j, s = ins * 64 + lane;
     unsigned off = 0x80000000u;
     if (ins < g.NI && s < 2 * g.RS) {
       const int hf = s >= g.RS ? 1 : 0, sl = s - hf * g.RS;
-      const int rr = fdiv(sl, g.fd_rp), cs = sl - rr * g.RP;
-      const int seg = rr / 6, r = rr - seg * 6;
+      const int seg = fdiv(sl, g.fd_ss), ss = sl - seg * g.SS;
+      const int r = fdiv(ss, g.fd_rp), cs = ss - r * g.RP;
       const int m5 = cs / 5, k5 = cs - 5 * m5, c = 4 * m5 + k5;
-      if (k5 < 4 && c < 4 * g.TC + 2) {
+      if (r < 6 && k5 < 4 && c < 4 * g.TC + 2) {
         const int R = R0 + seg, f = fdiv(R, g.fd_th), ty = R - f * g.TH;
         const int yy = 4 * ty - 1 + r, xx = 4 * tx0 - 1 + c;
         if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) off = (((f * H + yy) * W + xx) * C + hf * 4) * 4;
@@ -107,9 +114,9 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
   }
   auto issue_raw = [&](int k, int stage) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < W4_DPW; ++j) {
+    for (int j = 0; j < DPW; ++j) {
       const int ins = wid + W4_WAVES * j;
-      // every wave issues W4_DPW DMAs (wave-uniform vmcnt counts); those past NI land in the sink, the
+      // every wave issues DPW DMAs (wave-uniform vmcnt counts); those past NI land in the sink, the
       // ones past the last chunk re-read chunk 0
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           xr, (__attribute__((address_space(3))) void*)(ins < g.NI ? smem + stage * W4_STAGE + ins * 1024 : sink), 16,
@@ -121,7 +128,7 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
   const int t = lane & 15, k4 = lane >> 4;
   const int tv = t < NT ? t : 0;  // rows past the group's tiles compute tile 0 again (discarded)
   const int tseg = fdiv(tv, g.fd_tc), tcol = tv - tseg * g.TC;
-  const int lane_off = ((k4 >> 1) * g.RS + 6 * tseg * g.RP + 5 * tcol) * 16 + (k4 & 1) * 8;
+  const int lane_off = ((k4 >> 1) * g.RS + tseg * g.SS + 5 * tcol) * 16 + (k4 & 1) * 8;
   // B^T row i (Lavin F(4,3)) over window rows (r0..r3) with coefficients (c0..c3): wave-uniform
   int r0, r1, r2, r3;
   float c0, c1, c2, c3;
@@ -137,14 +144,21 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
   // v[j] = (B^T d B)[i][j] for the lane's tile and its two channels (.x: K step 0, .y: K step 1); the
   // column transform accumulates per window column (each row-pass value dies at once: registers)
   auto transform = [&](int stage, f32x2 (&v)[6]) __attribute__((always_inline)) {
+    if constexpr ((KO & 1) != 0) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) v[j] = f32x2{(float)(lane + j + stage), (float)(lane - j)};
+      return;
+    }
     const char* base = smem + stage * W4_STAGE + lane_off;
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
       const int co = (c + (c >> 2)) * 16;  // pixel columns 0..5 of the window -> slots 0,1,2,3,5,6
-      const f32x2 d0 = *reinterpret_cast<const f32x2*>(base + ro0 + co);
-      const f32x2 d1 = *reinterpret_cast<const f32x2*>(base + ro1 + co);
-      const f32x2 d2 = *reinterpret_cast<const f32x2*>(base + ro2 + co);
-      const f32x2 d3 = *reinterpret_cast<const f32x2*>(base + ro3 + co);
+      const char* b = base + co;
+      if constexpr ((KO & 16) != 0) asm volatile("" : "+v"(b));
+      const f32x2 d0 = *reinterpret_cast<const f32x2*>(b + ro0);
+      const f32x2 d1 = *reinterpret_cast<const f32x2*>(b + ro1);
+      const f32x2 d2 = *reinterpret_cast<const f32x2*>(b + ro2);
+      const f32x2 d3 = *reinterpret_cast<const f32x2*>(b + ro3);
       const f32x2 t = d0 * c0 + d1 * c1 + d2 * c2 + d3 * c3;
       // B^T columns: c0 (4,0,0,0,0,0) c1 (0,-4,4,-2,2,4) c2 (-5,-4,-4,-1,-1,0) c3 (0,1,-1,2,-2,-5)
       // c4 (1,1,1,1,1,0) c5 (0,0,0,0,0,1)
@@ -176,7 +190,7 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
   f32x4 u[3][3];
   f32x2 a[6];
 
-  // ---- prologue: raw(0), raw(1) and U(0) in flight. Per chunk every wave then issues exactly W4_DPW
+  // ---- prologue: raw(0), raw(1) and U(0) in flight. Per chunk every wave then issues exactly DPW
   // DMAs + 9 U loads (past-the-end ones re-read chunk 0), so the counted vmcnt waits are exact.
   issue_raw(0, 0);
   __builtin_amdgcn_sched_barrier(0);
@@ -195,13 +209,13 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
   auto step = [&](int k, int ph, bool first) __attribute__((always_inline)) {
     // own raw(k) landed: issued after it are U(k-1), raw(k+1), U(k) (k = 0: raw(1), U(0))
     if (first)
-      __builtin_amdgcn_s_waitcnt(vm_wait(W4_DPW + 9));
+      __builtin_amdgcn_s_waitcnt(vm_wait(DPW + 9));
     else
-      __builtin_amdgcn_s_waitcnt(vm_wait(W4_DPW + 18));
+      __builtin_amdgcn_s_waitcnt(vm_wait(DPW + 18));
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((KO & 32) == 0) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    issue_raw(k + 2, (ph + 2) % W4_NR);
+    if constexpr ((KO & 8) == 0) issue_raw(k + 2, (ph + 2) % W4_NR);
     __builtin_amdgcn_sched_barrier(0);
     transform(ph, a);
     __builtin_amdgcn_sched_barrier(0);
@@ -218,7 +232,8 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
                                                                0, 0);
           }
 #pragma unroll
-      for (int nt = 0; nt < 3; ++nt) u[nt][gg] = load_u(k + 1, nt, gg);
+      for (int nt = 0; nt < 3; ++nt)
+        if constexpr ((KO & 2) == 0) u[nt][gg] = load_u(k + 1, nt, gg);
     }
     // each group's 3 U reloads right after the 12 MFMAs that read those registers
 #pragma unroll
@@ -245,6 +260,15 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
   __builtin_amdgcn_s_waitcnt(vm_wait(0));  // past-the-end DMAs drained before LDS is reused
   __syncthreads();
 
+  if constexpr ((KO & 4) != 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+      for (int nt = 0; nt < 3; ++nt) sum += acc[j][nt][0] + acc[j][nt][1] + acc[j][nt][2] + acc[j][nt][3];
+    if (sum == 1234.5f) reinterpret_cast<float*>(p.y)[tid] = sum;
+    return;
+  }
   // ---- epilogue: wave i: R_i[b] = sum_j A^T[b][j] M[i][j] -> Z[i*4+b][co][tile]; then
   // Y[a][b] = sum_i A^T[a][i] R_i[b] per unit (tile, 4 channels, column b)
   float* Z = reinterpret_cast<float*>(smem);
@@ -287,8 +311,10 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
     y[2] = s12 + 4.f * s34;
     y[3] = d12 + 8.f * d34 + z[5];
     float* yout = reinterpret_cast<float*>(p.y);
+    if (xx >= W) continue;  // partial tiles at the right / bottom edge of maps with H, W % 4 != 0
 #pragma unroll
     for (int aa = 0; aa < 4; ++aa) {
+      if (4 * ty + aa >= H) break;
       f32x4 o = y[aa] + bias;
       if constexpr (RELU) {
 #pragma unroll
@@ -301,27 +327,28 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
   }
 }
 
-template <int NCH>
+template <int NCH, int DPW>
 hipError_t launch_w4(const ConvParams& p, const W4Geo& g, int n_blocks, hipStream_t s) {
   const dim3 grid(n_blocks), block(W4_THREADS);
   if (p.y_c8) {
     if (p.relu)
-      hipLaunchKernelGGL((conv_wino4<NCH, true, true>), grid, block, 0, s, p, g);
+      hipLaunchKernelGGL((conv_wino4<NCH, true, true, DPW>), grid, block, 0, s, p, g);
     else
-      hipLaunchKernelGGL((conv_wino4<NCH, true, false>), grid, block, 0, s, p, g);
+      hipLaunchKernelGGL((conv_wino4<NCH, true, false, DPW>), grid, block, 0, s, p, g);
   } else {
     if (p.relu)
-      hipLaunchKernelGGL((conv_wino4<NCH, false, true>), grid, block, 0, s, p, g);
+      hipLaunchKernelGGL((conv_wino4<NCH, false, true, DPW>), grid, block, 0, s, p, g);
     else
-      hipLaunchKernelGGL((conv_wino4<NCH, false, false>), grid, block, 0, s, p, g);
+      hipLaunchKernelGGL((conv_wino4<NCH, false, false, DPW>), grid, block, 0, s, p, g);
   }
   return hipGetLastError();
 }
 
-// Tile-group shape, patch pitch and DMA count for p (false: no group of >= 12 tiles fits).
+// Tile-group shape, patch pitches and DMA count for p (false: no group of >= 12 tiles fits). Tiles
+// past the map's right / bottom edge (H, W % 4 != 0) are computed on zero padding and not stored.
 bool wino4_geometry(const ConvParams& p, W4Geo* g, int* n_blocks) {
-  if (p.Ho % 4 || p.Wo % 4 || p.Cout % 48 || p.Cin % 8) return false;
-  const int TH = p.Ho / 4, TW = p.Wo / 4;
+  if (p.Cout % 48 || p.Cin % 8) return false;
+  const int TH = (p.Ho + 3) / 4, TW = (p.Wo + 3) / 4;
   const long rows = (long)p.N * p.To * TH;  // flattened tile rows
   int TC = 0;
   for (int d = TW < 16 ? TW : 16; d >= 1 && !TC; --d)
@@ -331,21 +358,24 @@ bool wino4_geometry(const ConvParams& p, W4Geo* g, int* n_blocks) {
     if (rows % d == 0) TR = d;
   if (TR * TC < 12) return false;
   const int PC = 4 * TC + 2, rp0 = (PC - 1) + (PC - 1) / 4 + 1;
-  // RP: fewest tiles sharing a bank quad (ds_read_b64: a 32-lane group = 16 tiles x 16 B), then smallest
-  int best_rp = 0, best_m = 99;
-  for (int rp = rp0; rp < rp0 + 16; ++rp) {
-    if ((2 * 6 * TR * rp + 63) / 64 > W4_WAVES * W4_DPW) break;
-    int cnt[16] = {0}, m = 0;
-    for (int t = 0; t < TR * TC; ++t) {
-      const int v = (6 * (t / TC) * rp + 5 * (t % TC)) & 15;
-      if (++cnt[v] > m) m = cnt[v];
+  // RP, SS: fewest tiles sharing a 16-B bank quad of a 256-B row (ds_read_b64: a 32-lane group = 16
+  // tiles x one channel pair), then the fewest DMA instructions
+  int best = 1 << 30;
+  for (int rp = rp0; rp < rp0 + 16; ++rp)
+    for (int ss = 6 * rp; ss < 6 * rp + 16; ++ss) {
+      const int ni = (2 * TR * ss + 63) / 64;
+      if (ni > W4_WAVES * W4_DPW_MAX) continue;
+      int cnt[16] = {0}, m = 0;
+      for (int t = 0; t < TR * TC; ++t) {
+        const int v = ((t / TC) * ss + 5 * (t % TC)) & 15;
+        if (++cnt[v] > m) m = cnt[v];
+      }
+      const int score = m * 1000 + ni;
+      if (score < best) best = score, g->RP = rp, g->SS = ss;
     }
-    if (m < best_m) best_m = m, best_rp = rp;
-  }
-  if (!best_rp) return false;
+  if (best == 1 << 30) return false;
   g->TR = TR, g->TC = TC, g->TH = TH, g->TW = TW;
-  g->RP = best_rp;
-  g->RS = 6 * TR * best_rp;
+  g->RS = TR * g->SS;
   g->NI = (2 * g->RS + 63) / 64;
   g->n_cob = p.Cout / 48;
   g->gpr = TW / TC;
@@ -353,7 +383,8 @@ bool wino4_geometry(const ConvParams& p, W4Geo* g, int* n_blocks) {
   g->fd_gpr = fast_div(g->gpr);
   g->fd_th = fast_div(TH);
   g->fd_tc = fast_div(TC);
-  g->fd_rp = fast_div(best_rp);
+  g->fd_rp = fast_div(g->RP);
+  g->fd_ss = fast_div(g->SS);
   *n_blocks = (int)(rows / TR) * g->gpr * g->n_cob;
   return true;
 }
@@ -376,9 +407,11 @@ hipError_t launch_wino4(const ConvParams& p, hipStream_t s) {
   int nb;
   wino4_geometry(p, &g, &nb);
   switch (p.Cin >> 3) {
-    case 8: return launch_w4<8>(p, g, nb, s);
-    case 16: return launch_w4<16>(p, g, nb, s);
-    default: return launch_w4<0>(p, g, nb, s);
+    // (launch_w4 called from this non-template function: instantiated from inside another template,
+    // hipcc left the kernels' host stubs undefined)
+    case 8: return g.NI <= W4_WAVES * 3 ? launch_w4<8, 3>(p, g, nb, s) : launch_w4<8, 4>(p, g, nb, s);
+    case 16: return g.NI <= W4_WAVES * 3 ? launch_w4<16, 3>(p, g, nb, s) : launch_w4<16, 4>(p, g, nb, s);
+    default: return g.NI <= W4_WAVES * 3 ? launch_w4<0, 3>(p, g, nb, s) : launch_w4<0, 4>(p, g, nb, s);
   }
 }
 
@@ -417,3 +450,35 @@ void wino4_transform_weights(const double* w, int cout, int cin, int cout_p, int
         }
     }
 }
+
+#ifdef CLASFV_KNOCKOUTS
+// tools/convbench: conv_wino4 timing knock-outs (KO bits above) on 8-chunk maps (layer1), channels-last
+// output with ReLU.
+template <int KO>
+static hipError_t launch_w4ko(const ConvParams& p, const W4Geo& g, int nb, hipStream_t s) {
+  if (p.Cin == 128)
+    hipLaunchKernelGGL((conv_wino4<16, false, true, 3, KO>), dim3(nb), dim3(W4_THREADS), 0, s, p, g);
+  else
+    hipLaunchKernelGGL((conv_wino4<8, false, true, 3, KO>), dim3(nb), dim3(W4_THREADS), 0, s, p, g);
+  return hipGetLastError();
+}
+hipError_t launch_wino4_ko(const ConvParams& p, hipStream_t s, int ko) {
+  W4Geo g;
+  int nb;
+  if (!wino4_supported(p) || (p.Cin != 64 && p.Cin != 128) || p.y_c8 || !p.relu || !wino4_geometry(p, &g, &nb) || g.NI > 18)
+    return hipErrorInvalidValue;
+  switch (ko) {
+    case 0: return launch_w4ko<0>(p, g, nb, s);
+    case 1: return launch_w4ko<1>(p, g, nb, s);
+    case 2: return launch_w4ko<2>(p, g, nb, s);
+    case 3: return launch_w4ko<3>(p, g, nb, s);
+    case 4: return launch_w4ko<4>(p, g, nb, s);
+    case 8: return launch_w4ko<8>(p, g, nb, s);
+    case 15: return launch_w4ko<15>(p, g, nb, s);
+    case 16: return launch_w4ko<16>(p, g, nb, s);
+    case 32: return launch_w4ko<32>(p, g, nb, s);
+    case 47: return launch_w4ko<47>(p, g, nb, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+#endif

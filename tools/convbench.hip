@@ -18,6 +18,7 @@
 hipError_t launch_wino_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko);
+hipError_t launch_wino4_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winor_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
 hipError_t launch_patch_bf16_v1(const ConvParams& p, hipStream_t s);
@@ -130,7 +131,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   auto launch = [&](int ko) {
-    if (wino4) CK(launch_wino4(p, s));
+    if (wino4) CK(ko ? launch_wino4_ko(p, s, ko) : launch_wino4(p, s));
     else if (winor) CK(launch_winor_ko(p, s, ko));
     else if (winoqp) CK(launch_winoq_probe(p, s, ko));
     else if (winoq) CK(launch_winoq_ko(p, s, ko));
