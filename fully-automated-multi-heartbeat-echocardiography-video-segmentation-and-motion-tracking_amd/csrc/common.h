@@ -95,8 +95,10 @@ bool wino4_supported(const ConvParams& p);
 hipError_t launch_wino4(const ConvParams& p, hipStream_t s);
 // MFMA work (GFLOP) one conv_wino4 launch executes (16 MFMA rows per tile group, padding included).
 double wino4_exec_gflop(const ConvParams& p);
-// U[cout_p/48][cin_p/8][6][3][3][64][4] from folded weights w[cout][cin][3][3] (double).
+// conv_wino4's transformed weights (wino4_weight_floats(cin_p, cout_p) floats) from folded weights
+// w[cout][cin][3][3] (double).
 void wino4_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
+size_t wino4_weight_floats(int cin_p, int cout_p);
 // Fused Winograd F(4,3)-in-time path for stride-1 3x1x1 fp32 convs; p.w = transformed weights.
 bool winot_supported(const ConvParams& p);
 hipError_t launch_winot(const ConvParams& p, hipStream_t s);

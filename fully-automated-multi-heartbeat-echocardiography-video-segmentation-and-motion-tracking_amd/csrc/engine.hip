@@ -645,7 +645,7 @@ int clasfv_finalize(clasfv_t h) {
       wino_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, u.data());
       if ((rc = upload(u, &c.dwino))) return rc;
       if (c.cout_p % 48 == 0 && c.cin_p % 8 == 0) {
-        std::vector<float> u4((size_t)36 * c.cin_p * c.cout_p);
+        std::vector<float> u4(wino4_weight_floats(c.cin_p, c.cout_p));
         wino4_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, u4.data());
         if ((rc = upload(u4, &c.dwino4))) return rc;
       }

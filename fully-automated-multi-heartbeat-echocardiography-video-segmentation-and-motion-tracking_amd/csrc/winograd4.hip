@@ -9,32 +9,50 @@
 // tools/wino44_precision.py: through the whole network the fp32 F(4x4) logits are within 9e-6 of a
 // float64 forward (F(2x2): 8e-6, direct fp32: 7e-6).
 //
-// Block = 6 waves x one tile group (TR x TC <= 16 tiles, the MFMA M rows) x 48 output channels. Wave i
-// owns the Winograd-domain row i (elements (i, 0..5)) and builds its A operands itself: a lane (tile
-// t = lane % 16, channel pair k4 = lane / 16) reads the 4 window rows B^T row i touches straight from
-// the raw patch (ds_read_b64 = the two input channels of the chunk's two K steps), applies B^T row i,
-// then the column transform, and the results ARE its MFMA A registers -- no V tensor through LDS and
-// no V barrier (conv_wino_q's limiter). The raw patch of a chunk (8 channels) is
-// LDS-DMA'd once per block into a 3-stage ring (one barrier per chunk); U streams from L2 into
-// registers one chunk ahead, each register reloaded right after its last MFMA of the chunk (the
-// loads then have a whole chunk to land). Epilogue: wave i folds its row with A^T (6 -> 4 values per
-// tile and channel), the rows meet in LDS, and Y = A^T (.) with bias and ReLU is stored channels-last
-// or 8-channel-blocked (the temporal consumer's layout, engine.hip c8_pair).
+// Block = 4 waves x one tile group (TR x TC <= 16 tiles, the MFMA M rows) x 48 output channels, two
+// blocks per CU (one wave of each per SIMD: 6-wave blocks land 2,2,1,1 on the SIMDs and cap even a
+// pure MFMA stream at 0.67-0.73 of peak, tools/occ_probe.hip; 4-wave blocks reach 0.93). Wave
+// (rh, ch) owns the 3 x 3 quadrant of Winograd-domain elements (3 rh + r, 3 ch + jj) and builds its
+// own A operands: a lane (tile t = lane % 16, channel pair k4 = lane / 16) reads the 5 window rows
+// its B^T rows touch straight from the raw patch (ds_read_b64 = the two input channels of the
+// chunk's two K steps), applies its 3 B^T rows, then its 3 columns of the column transform; the
+// results ARE its MFMA A registers -- no V tensor through LDS and no V barrier (conv_wino_q's
+// limiter). The raw patch of a chunk (8 channels) is LDS-DMA'd once per block
+// into a ring (one barrier per chunk, or per 2 chunks with a 4-stage ring); U streams from L2 into
+// registers one chunk ahead, each register reloaded right after the MFMAs that read it (the loads
+// then have a whole chunk to land). On gfx950 the f32 VALU and the f32 MFMA share one rate, so the
+// transforms' packed-f32 work is priced in MFMA cycles (about 15 % of them). Epilogue, per 16
+// output channels: each wave folds its 3 columns with A^T (the distinct partial sums only), the
+// halves meet in LDS, and Y = A^T (.) A with bias and ReLU is stored channels-last or
+// 8-channel-blocked (the temporal consumer's layout, engine.hip c8_pair).
 #include "common.h"
+
+#include <type_traits>
 
 namespace {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int W4_WAVES = 6;
+constexpr int W4_WAVES = 4;
 constexpr int W4_THREADS = 64 * W4_WAVES;
-constexpr int W4_DPW_MAX = 4;                        // LDS-DMA instructions per wave per chunk (3 or 4)
-constexpr int W4_STAGE = W4_WAVES * W4_DPW_MAX * 1024;  // 24 KB raw stage (<= 24 x 64 16-B slots used)
-constexpr int W4_NR = 3;                                // raw ring stages
-constexpr int W4_ZS = 48 * 17 + 1;                   // epilogue plane [co (stride 17)][tile (16)], odd
-constexpr int W4_LDS = 24 * W4_ZS * 4;               // 78,432 B: Z[i*4+b] planes; ring + sink inside
-static_assert(W4_NR * W4_STAGE + 1024 <= W4_LDS, "ring and sink fit under the epilogue planes");
-static_assert(2 * W4_LDS <= 160 * 1024, "two blocks per CU");
+constexpr int W4_NU = 14;  // U f32x4 loads per wave per chunk (54 B operands + 2 pad)
+// raw ring for DPW DMA instructions per wave per chunk (stage = 4 DPW KB): DPW = 4 (<= 16 per stage):
+// 4 stages, one barrier per 2 chunks; DPW = 5, 6: 3 stages, one barrier per chunk
+template <int DPW>
+struct W4Ring {
+  static constexpr int STAGE = W4_WAVES * DPW * 1024;
+  static constexpr int NR = DPW == 4 ? 4 : 3;
+  static constexpr int STEP = NR - 2;  // chunks per barrier
+  static constexpr int LDS = NR * STAGE + 1024;  // + sink
+};
+// epilogue planes per 16 output channels: 18 column-half-0 planes [i][3] then 24 column-half-1 planes
+// [i][4 (b)], each [co (stride W4_CS)][tile (16)] (a lane's 4 tiles = one 16-B store)
+constexpr int W4_CS = 20;
+constexpr int W4_ZS = 16 * W4_CS + 4;
+constexpr int W4_ZBYTES = 42 * W4_ZS * 4;  // 54,432 B
+static_assert(W4_ZBYTES <= W4Ring<4>::LDS && W4Ring<4>::LDS <= 80 * 1024 && W4Ring<5>::LDS <= 80 * 1024 &&
+                  W4Ring<6>::LDS <= 80 * 1024,
+              "two blocks per CU");
 
 __device__ inline int xcd_swizzle4(int b, int nb) {
   const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
@@ -56,7 +74,7 @@ struct W4Geo {
   int RP;       // 16-B LDS slots per raw patch row (a pad slot after every 4 pixels: bank spread)
   int SS;       // slots per segment (>= 6 RP: free slots shift the next segment's banks)
   int RS;       // slots per channel-half region (TR SS); region 1 = input channels 4..7
-  int NI;       // DMA wave-instructions carrying data per stage (<= 6 DPW)
+  int NI;       // DMA wave-instructions carrying data per stage (<= 4 DPW)
   int n_cob;    // 48-channel output blocks
   int gpr;      // groups per flattened tile row (TW / TC)
   FastDiv fd_cob, fd_gpr, fd_th, fd_tc, fd_rp, fd_ss;
@@ -64,16 +82,50 @@ struct W4Geo {
 
 namespace {
 
+// One row half of the input transform: t[r] = (B^T d)[3 rh + r][column] from the 5 window rows
+// e[q] = d[rh + q] (Lavin's B^T rows 0-2 read d rows 0-4, rows 3-5 read d rows 1-5).
+template <int RH>
+__device__ inline void bt_rows(const f32x2 (&e)[5], f32x2 (&t)[3]) {
+  if constexpr (RH == 0) {
+    t[0] = e[0] * 4.f - e[2] * 5.f + e[4];
+    const f32x2 s = e[1] + e[2], u = e[3] + e[4], d = e[1] - e[2], w = e[4] - e[3];
+    t[1] = u - s * 4.f;
+    t[2] = w + d * 4.f;
+  } else {
+    const f32x2 x = e[3] - e[1], y = e[2] - e[0];
+    t[0] = x + y * 2.f;
+    t[1] = x - y * 2.f;
+    t[2] = e[0] * 4.f - e[2] * 5.f + e[4];
+  }
+}
+
+// One column half of the input transform: v[jj] = sum_c t[c] B^T[3 ch + jj][c].
+template <int CH>
+__device__ inline void bt_cols(const f32x2 (&t)[6], f32x2 (&v)[3]) {
+  if constexpr (CH == 0) {
+    v[0] = t[0] * 4.f - t[2] * 5.f + t[4];
+    const f32x2 s = t[1] + t[2], u = t[3] + t[4], d = t[1] - t[2], w = t[4] - t[3];
+    v[1] = u - s * 4.f;
+    v[2] = w + d * 4.f;
+  } else {
+    const f32x2 x = t[4] - t[2], y = t[3] - t[1];
+    v[0] = x + y * 2.f;
+    v[1] = x - y * 2.f;
+    v[2] = t[1] * 4.f - t[3] * 5.f + t[5];
+  }
+}
+
 // NCH: input-channel chunks (8 channels each; 0 = runtime). C8: 8-channel-blocked output. DPW: DMA
-// instructions per wave per chunk (3: <= 18 per stage; 4: the 8-segment groups of 7x7 maps). KO: timing
-// knock-outs for tools/convbench (0 in the product; results are wrong otherwise): 1 no transform
-// reads / VALU, 2 no U reloads, 4 no epilogue, 8 no DMAs in the chunk loop; 16 (a variant, correct):
-// every window column read from its own address register (no ds_read2_b64 pairing); 32 no chunk barrier.
+// instructions per wave per chunk (W4Ring). KO: timing knock-outs for tools/convbench (0 in the product;
+// results are wrong otherwise): 1 no transform reads / VALU, 2 no U reloads, 4 no epilogue, 8 no DMAs
+// in the chunk loop, 32 no chunk barrier; 64 n: the first round's second blocks sleep n x 8128 cycles.
 template <int NCH, bool C8, bool RELU, int DPW, int KO = 0>
-__global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_wino4(ConvParams p,
+__global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino4(ConvParams p,
                                                                                                      W4Geo g) {
-  __shared__ __align__(16) char smem[W4_LDS];
-  char* sink = smem + W4_NR * W4_STAGE;
+  using RG = W4Ring<DPW>;
+  constexpr int NR = RG::NR, STAGE = RG::STAGE;
+  __shared__ __align__(16) char smem[RG::LDS];
+  char* sink = smem + NR * STAGE;
 
   // buffer descriptors (wave-uniform bases): 32-bit per-lane offsets, no 64-bit address VGPRs; an
   // out-of-range offset reads zeros (the padding pixels)
@@ -89,12 +141,10 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
   const int nchunk = NCH > 0 ? NCH : C >> 3;
   const int NT = g.TR * g.TC;
 
-  // ---- LDS-DMA slot table: instruction j of this wave fills slots s = (wid + 6 j) * 64 + lane of a
+  // ---- LDS-DMA slot table: instruction j of this wave fills slots s = (wid + 4 j) * 64 + lane of a
   // stage; s < RS: input channels 0..3 of a pixel, else 4..7; within a region slot = seg * SS + r * RP
   // + cs (window row r < 6 of segment seg), pixel column c = cs - cs / 5 (cs % 5 == 4: pad)
-  // (array sized by a constant: a template-dependent bound captured by the lambdas below left the
-  // kernels' host stubs undefined under hipcc)
-  unsigned d_off[W4_DPW_MAX];  // byte offset of the slot's 16 B in chunk 0, or 0x80000000 (zeros)
+  unsigned d_off[6];  // byte offset of the slot's 16 B in chunk 0, or 0x80000000 (zeros)
 #pragma unroll
   for (int j = 0; j < DPW; ++j) {
     const int ins = wid + W4_WAVES * j, s = ins * 64 + lane;
@@ -119,210 +169,233 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3
       // every wave issues DPW DMAs (wave-uniform vmcnt counts); those past NI land in the sink, the
       // ones past the last chunk re-read chunk 0
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          xr, (__attribute__((address_space(3))) void*)(ins < g.NI ? smem + stage * W4_STAGE + ins * 1024 : sink), 16,
+          xr, (__attribute__((address_space(3))) void*)(ins < g.NI ? smem + stage * STAGE + ins * 1024 : sink), 16,
           d_off[j], k < nchunk ? k * 32 : 0, 0, 0);
     }
   };
 
   // ---- transform lane: tile t (MFMA row), channel pair k4 (MFMA K index) -> region k4 / 2, 8-B half k4 % 2
+  const int rh = wid >> 1, ch = wid & 1;
   const int t = lane & 15, k4 = lane >> 4;
   const int tv = t < NT ? t : 0;  // rows past the group's tiles compute tile 0 again (discarded)
   const int tseg = fdiv(tv, g.fd_tc), tcol = tv - tseg * g.TC;
-  const int lane_off = ((k4 >> 1) * g.RS + tseg * g.SS + 5 * tcol) * 16 + (k4 & 1) * 8;
-  // B^T row i (Lavin F(4,3)) over window rows (r0..r3) with coefficients (c0..c3): wave-uniform
-  int r0, r1, r2, r3;
-  float c0, c1, c2, c3;
-  switch (wid) {
-    case 0: r0 = 0, r1 = 2, r2 = 4, r3 = 4, c0 = 4.f, c1 = -5.f, c2 = 1.f, c3 = 0.f; break;
-    case 1: r0 = 1, r1 = 2, r2 = 3, r3 = 4, c0 = -4.f, c1 = -4.f, c2 = 1.f, c3 = 1.f; break;
-    case 2: r0 = 1, r1 = 2, r2 = 3, r3 = 4, c0 = 4.f, c1 = -4.f, c2 = -1.f, c3 = 1.f; break;
-    case 3: r0 = 1, r1 = 2, r2 = 3, r3 = 4, c0 = -2.f, c1 = -1.f, c2 = 2.f, c3 = 1.f; break;
-    case 4: r0 = 1, r1 = 2, r2 = 3, r3 = 4, c0 = 2.f, c1 = -1.f, c2 = -2.f, c3 = 1.f; break;
-    default: r0 = 1, r1 = 3, r2 = 5, r3 = 5, c0 = 4.f, c1 = -5.f, c2 = 1.f, c3 = 0.f; break;
-  }
-  const int ro0 = r0 * g.RP * 16, ro1 = r1 * g.RP * 16, ro2 = r2 * g.RP * 16, ro3 = r3 * g.RP * 16;
-  // v[j] = (B^T d B)[i][j] for the lane's tile and its two channels (.x: K step 0, .y: K step 1); the
-  // column transform accumulates per window column (each row-pass value dies at once: registers)
-  auto transform = [&](int stage, f32x2 (&v)[6]) __attribute__((always_inline)) {
+  const int lane_off = ((k4 >> 1) * g.RS + tseg * g.SS + rh * g.RP + 5 * tcol) * 16 + (k4 & 1) * 8;
+  const int rp16 = g.RP * 16;
+  // a[r][jj] = (B^T d B)[3 rh + r][3 ch + jj] for the lane's tile and its two channels (.x: K step 0,
+  // .y: K step 1). One straight-line body per quadrant (a wave-uniform switch per chunk): the 30 reads
+  // are scheduled ahead of their arithmetic instead of waiting column by column.
+  auto transform = [&](int stage, f32x2 (&a)[3][3]) __attribute__((always_inline)) {
     if constexpr ((KO & 1) != 0) {
 #pragma unroll
-      for (int j = 0; j < 6; ++j) v[j] = f32x2{(float)(lane + j + stage), (float)(lane - j)};
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) a[r][jj] = f32x2{(float)(lane + 3 * r + jj + stage), (float)(lane - jj)};
       return;
     }
-    const char* base = smem + stage * W4_STAGE + lane_off;
+    const char* base = smem + stage * STAGE + lane_off;
+    auto body = [&](auto rh_c, auto ch_c) __attribute__((always_inline)) {
+      constexpr int RH = decltype(rh_c)::value, CH = decltype(ch_c)::value;
+      f32x2 tt[3][6];
 #pragma unroll
-    for (int c = 0; c < 6; ++c) {
-      const int co = (c + (c >> 2)) * 16;  // pixel columns 0..5 of the window -> slots 0,1,2,3,5,6
-      const char* b = base + co;
-      if constexpr ((KO & 16) != 0) asm volatile("" : "+v"(b));
-      const f32x2 d0 = *reinterpret_cast<const f32x2*>(b + ro0);
-      const f32x2 d1 = *reinterpret_cast<const f32x2*>(b + ro1);
-      const f32x2 d2 = *reinterpret_cast<const f32x2*>(b + ro2);
-      const f32x2 d3 = *reinterpret_cast<const f32x2*>(b + ro3);
-      const f32x2 t = d0 * c0 + d1 * c1 + d2 * c2 + d3 * c3;
-      // B^T columns: c0 (4,0,0,0,0,0) c1 (0,-4,4,-2,2,4) c2 (-5,-4,-4,-1,-1,0) c3 (0,1,-1,2,-2,-5)
-      // c4 (1,1,1,1,1,0) c5 (0,0,0,0,0,1)
-      switch (c) {
-        case 0: v[0] = t * 4.f; break;
-        case 1: v[1] = t * -4.f, v[2] = t * 4.f, v[3] = t * -2.f, v[4] = t * 2.f, v[5] = t * 4.f; break;
-        case 2: v[0] += t * -5.f, v[1] += t * -4.f, v[2] += t * -4.f, v[3] -= t, v[4] -= t; break;
-        case 3: v[1] += t, v[2] -= t, v[3] += t * 2.f, v[4] += t * -2.f, v[5] += t * -5.f; break;
-        case 4: v[0] += t, v[1] += t, v[2] += t, v[3] += t, v[4] += t; break;
-        default: v[5] += t; break;
+      for (int c = 0; c < 6; ++c) {
+        const int co = (c + (c >> 2)) * 16;  // pixel columns 0..5 of the window -> slots 0,1,2,3,5,6
+        f32x2 e[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) e[q] = *reinterpret_cast<const f32x2*>(base + q * rp16 + co);
+        f32x2 t3[3];
+        bt_rows<RH>(e, t3);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) tt[r][c] = t3[r];
       }
+#pragma unroll
+      for (int r = 0; r < 3; ++r) bt_cols<CH>(tt[r], a[r]);
+    };
+    switch (wid) {
+      case 0: body(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}); break;
+      case 1: body(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}); break;
+      case 2: body(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{}); break;
+      default: body(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}); break;
     }
   };
 
-  // ---- U operands: [cob][chunk][i][nt][gg][lane][4], component m = 4 gg + comp <-> (j, ks) = (m / 2, m % 2)
+  // ---- U operands: [cob][chunk][wave][14][lane][4]; component m = 4 g + comp <-> MFMA (r, ks, nt, jj),
+  // m = ((r * 2 + ks) * 3 + nt) * 3 + jj (m >= 54: zero pad)
   const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(reinterpret_cast<const float*>(p.w) + ((size_t)cob * nchunk * W4_WAVES + wid) * 2304), (short)0,
-      nchunk * W4_WAVES * 2304 * 4, 0x00020000);
-  auto load_u = [&](int k, int nt, int gg) __attribute__((always_inline)) {
-    return __builtin_bit_cast(
-        f32x4, __builtin_amdgcn_raw_buffer_load_b128(ur, lane * 16, ((k < nchunk ? k : 0) * (W4_WAVES * 2304) + (nt * 3 + gg) * 256) * 4, 0));
+      const_cast<float*>(reinterpret_cast<const float*>(p.w) + ((size_t)cob * nchunk * W4_WAVES + wid) * (W4_NU * 256)),
+      (short)0, nchunk * W4_WAVES * W4_NU * 256 * 4, 0x00020000);
+  auto load_u = [&](int k, int gi) __attribute__((always_inline)) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         ur, lane * 16, ((k < nchunk ? k : 0) * (W4_WAVES * W4_NU * 256) + gi * 256) * 4, 0));
   };
 
-  f32x4 acc[6][3];
+  f32x4 acc[3][3][3];  // [r][jj][nt]
 #pragma unroll
-  for (int j = 0; j < 6; ++j)
+  for (int r = 0; r < 3; ++r)
 #pragma unroll
-    for (int nt = 0; nt < 3; ++nt) acc[j][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 u[3][3];
-  f32x2 a[6];
+    for (int jj = 0; jj < 3; ++jj)
+#pragma unroll
+      for (int nt = 0; nt < 3; ++nt) acc[r][jj][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 u[W4_NU];
+  f32x2 a[3][3];
 
+  if constexpr ((KO & 64) != 0) {  // stagger probe: the second block of each CU in the first round starts late
+    if (blockIdx.x >= 256 && blockIdx.x < 512)
+      for (int i = 0; i < KO / 64; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   // ---- prologue: raw(0), raw(1) and U(0) in flight. Per chunk every wave then issues exactly DPW
-  // DMAs + 9 U loads (past-the-end ones re-read chunk 0), so the counted vmcnt waits are exact.
+  // DMAs + 14 U loads (past-the-end ones re-read chunk 0), so the counted vmcnt waits are exact.
   issue_raw(0, 0);
   __builtin_amdgcn_sched_barrier(0);
   issue_raw(1, 1);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int nt = 0; nt < 3; ++nt)
-#pragma unroll
-    for (int gg = 0; gg < 3; ++gg) u[nt][gg] = load_u(0, nt, gg);
+  for (int gi = 0; gi < W4_NU; ++gi) u[gi] = load_u(0, gi);
   __builtin_amdgcn_sched_barrier(0);
 
-  // chunk k (ph = k % 3, compile time: ring stages are immediates): raw(k+2) DMA'd into stage
-  // (k+2) % 3 once every wave is past raw(k-1)'s reads; A(k) transformed from stage k % 3 straight
-  // into registers; MFMAs on A(k) x U(k), U(k+1) reloaded behind them. Other waves of the SIMD (3 per
-  // SIMD, two blocks per CU) fill the matrix pipe while a wave transforms.
+  // chunk k (ph = k % NR, compile time: ring stages are immediates). Every STEP chunks (a barrier):
+  // raw(k+2) .. raw(k+NR-1) DMA'd into the stages of chunks k-STEP .. k-1, which every wave has read
+  // once it is past the barrier. A(k) transformed from stage ph straight into registers; MFMAs on
+  // A(k) x U(k), U(k+1) reloaded behind them; the other block's wave on the SIMD fills the matrix
+  // pipe while this one transforms.
   auto step = [&](int k, int ph, bool first) __attribute__((always_inline)) {
-    // own raw(k) landed: issued after it are U(k-1), raw(k+1), U(k) (k = 0: raw(1), U(0))
-    if (first)
-      __builtin_amdgcn_s_waitcnt(vm_wait(DPW + 9));
-    else
-      __builtin_amdgcn_s_waitcnt(vm_wait(DPW + 18));
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr ((KO & 32) == 0) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr ((KO & 8) == 0) issue_raw(k + 2, (ph + 2) % W4_NR);
+    if (ph % RG::STEP == 0) {
+      // own raw(k) .. raw(k+STEP-1) landed: issued after them are the U loads of the STEP chunks
+      // before k (NR = 3 also raw(k+1)); first: U(0) only (NR = 3: raw(1), U(0))
+      constexpr int AFTER = NR == 3 ? DPW + W4_NU : W4_NU;
+      if (first)
+        __builtin_amdgcn_s_waitcnt(vm_wait(AFTER));
+      else
+        __builtin_amdgcn_s_waitcnt(vm_wait(AFTER + W4_NU));
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((KO & 32) == 0) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((KO & 8) == 0) {
+#pragma unroll
+        for (int d = 2; d < NR; ++d) issue_raw(k + d, (ph + d) % NR);
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
     transform(ph, a);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int gg = 0; gg < 3; ++gg) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int nt = 0; nt < 3; ++nt)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) {
-            const int j = 2 * gg + jj;
-            acc[j][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ks ? a[j].y : a[j].x, u[nt][gg][2 * jj + ks], acc[j][nt], 0,
-                                                               0, 0);
-          }
-#pragma unroll
-      for (int nt = 0; nt < 3; ++nt)
-        if constexpr ((KO & 2) == 0) u[nt][gg] = load_u(k + 1, nt, gg);
+    for (int m = 0; m < 54; ++m) {
+      const int jj = m % 3, nt = (m / 3) % 3, ks = (m / 9) % 2, r = m / 18;
+      acc[r][jj][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ks ? a[r][jj].y : a[r][jj].x, u[m >> 2][m & 3],
+                                                            acc[r][jj][nt], 0, 0, 0);
+      if ((m & 3) == 3 || m == 53) {
+        if constexpr ((KO & 2) == 0) u[m >> 2] = load_u(k + 1, m >> 2);
+      }
     }
-    // each group's 3 U reloads right after the 12 MFMAs that read those registers
+    if constexpr ((KO & 2) == 0) u[W4_NU - 1] = load_u(k + 1, W4_NU - 1);  // (the all-pad group: count only)
+    // each group's reload right after the 4 MFMAs that read it
 #pragma unroll
-    for (int gg = 0; gg < 3; ++gg) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);  // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);   // VMEM read
+    for (int gi = 0; gi < W4_NU - 2; ++gi) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
     }
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
   };
   if constexpr (NCH > 0) {
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) step(k, k % W4_NR, k == 0);
+    for (int k = 0; k < NCH; ++k) step(k, k % NR, k == 0);
   } else {
-    step(0, 0, true);
-    int k = 1;
+    // one ring revolution per loop trip (a fully unrolled runtime-length loop is not possible)
+#pragma unroll
+    for (int k = 0; k < NR - 1; ++k)
+      if (k < nchunk) step(k, k, k == 0);
+    int k = NR - 1;
 #pragma unroll 1
-    for (; k + 3 <= nchunk; k += 3) {
-      step(k, 1, false);
-      step(k + 1, 2, false);
-      step(k + 2, 0, false);
+    for (; k + NR <= nchunk; k += NR) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) step(k + i, (NR - 1 + i) % NR, false);
     }
-    if (k < nchunk) step(k, 1, false);
-    if (k + 1 < nchunk) step(k + 1, 2, false);
+#pragma unroll
+    for (int i = 0; i < NR - 1; ++i)
+      if (k + i < nchunk) step(k + i, (NR - 1 + i) % NR, false);
   }
-  __builtin_amdgcn_s_waitcnt(vm_wait(0));  // past-the-end DMAs drained before LDS is reused
-  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(vm_wait(0));  // past-the-end DMAs and U loads drained before LDS is reused
 
   if constexpr ((KO & 4) != 0) {
     float sum = 0.f;
 #pragma unroll
-    for (int j = 0; j < 6; ++j)
+    for (int r = 0; r < 3; ++r)
 #pragma unroll
-      for (int nt = 0; nt < 3; ++nt) sum += acc[j][nt][0] + acc[j][nt][1] + acc[j][nt][2] + acc[j][nt][3];
+      for (int jj = 0; jj < 3; ++jj)
+#pragma unroll
+        for (int nt = 0; nt < 3; ++nt)
+          sum += acc[r][jj][nt][0] + acc[r][jj][nt][1] + acc[r][jj][nt][2] + acc[r][jj][nt][3];
     if (sum == 1234.5f) reinterpret_cast<float*>(p.y)[tid] = sum;
     return;
   }
-  // ---- epilogue: wave i: R_i[b] = sum_j A^T[b][j] M[i][j] -> Z[i*4+b][co][tile]; then
-  // Y[a][b] = sum_i A^T[a][i] R_i[b] per unit (tile, 4 channels, column b)
+  // ---- epilogue, per 16 output channels nt: wave (rh, ch) stores the column partial sums of its rows
+  // i = 3 rh + r, P[i][b] = sum_j A^T[b][j] M[i][j] = E[e(b)] + F[b]: ch 0 the distinct E = (m0+m1+m2,
+  // m1-m2, m1+m2) (e(b) = 0, 1, 2, 1), ch 1 F = (m3+m4, 2(m3-m4), 4(m3+m4), 8(m3-m4)+m5); a thread then
+  // owns one unit (tile, 4 channels, column b) and stores Y[a][b] = sum_i A^T[a][i] P[i][b], a = 0..3.
   float* Z = reinterpret_cast<float*>(smem);
   const int q = lane >> 4, l16 = lane & 15;
-#pragma unroll
-  for (int nt = 0; nt < 3; ++nt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float m0 = acc[0][nt][r], m1 = acc[1][nt][r], m2 = acc[2][nt][r];
-      const float m3 = acc[3][nt][r], m4 = acc[4][nt][r], m5 = acc[5][nt][r];
-      const float s12 = m1 + m2, d12 = m1 - m2, s34 = m3 + m4, d34 = m3 - m4;
-      float* zp = Z + (wid * 4) * W4_ZS + (16 * nt + l16) * 17 + 4 * q + r;
-      zp[0 * W4_ZS] = m0 + s12 + s34;
-      zp[1 * W4_ZS] = d12 + 2.f * d34;
-      zp[2 * W4_ZS] = s12 + 4.f * s34;
-      zp[3 * W4_ZS] = d12 + 8.f * d34 + m5;
-    }
-  __syncthreads();
-  const int nunits = NT * 48;
   const size_t plane = (size_t)p.N * p.To * H * W * 8;
+  float* yout = reinterpret_cast<float*>(p.y);
+  const int ub = tid & 3, ucq = (tid >> 2) & 3, utile = tid >> 4;  // this thread's unit
+  const int useg = fdiv(utile, g.fd_tc), utc = utile - useg * g.TC;
+  const int uR = R0 + useg, uf = fdiv(uR, g.fd_th), uty = uR - uf * g.TH;
+  const int uxx = 4 * (tx0 + utc) + ub;
+  const bool ulive = utile < NT && uxx < W;
 #pragma unroll
-  for (int rnd = 0; rnd < 2; ++rnd) {
-    const int un = tid + W4_THREADS * rnd;
-    if (un >= nunits) break;
-    const int b = un & 3, rest = un >> 2, tile = rest / 12, cq = rest - tile * 12;
-    f32x4 z[6];
+  for (int nt = 0; nt < 3; ++nt) {
+    __syncthreads();  // the ring (nt = 0) / the previous pass's planes are no longer read
+    if (ch == 0) {
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const float* zp = Z + (i * 4 + b) * W4_ZS + (4 * cq) * 17 + tile;
-      z[i] = f32x4{zp[0], zp[17], zp[34], zp[51]};
-    }
-    const int seg = fdiv(tile, g.fd_tc), tc = tile - seg * g.TC;
-    const int R = R0 + seg, f = fdiv(R, g.fd_th), ty = R - f * g.TH;
-    const int xx = 4 * (tx0 + tc) + b, co = cob * 48 + 4 * cq;
-    const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const f32x4 s12 = z[1] + z[2], d12 = z[1] - z[2], s34 = z[3] + z[4], d34 = z[3] - z[4];
-    f32x4 y[4];
-    y[0] = z[0] + s12 + s34;
-    y[1] = d12 + 2.f * d34;
-    y[2] = s12 + 4.f * s34;
-    y[3] = d12 + 8.f * d34 + z[5];
-    float* yout = reinterpret_cast<float*>(p.y);
-    if (xx >= W) continue;  // partial tiles at the right / bottom edge of maps with H, W % 4 != 0
-#pragma unroll
-    for (int aa = 0; aa < 4; ++aa) {
-      if (4 * ty + aa >= H) break;
-      f32x4 o = y[aa] + bias;
-      if constexpr (RELU) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
+      for (int r = 0; r < 3; ++r) {
+        const f32x4 m0 = acc[r][0][nt], m1 = acc[r][1][nt], m2 = acc[r][2][nt];
+        f32x4* zp = reinterpret_cast<f32x4*>(Z + ((3 * rh + r) * 3) * W4_ZS + l16 * W4_CS + 4 * q);
+        zp[0] = m0 + m1 + m2;
+        zp[W4_ZS / 4] = m1 - m2;
+        zp[2 * W4_ZS / 4] = m1 + m2;
       }
-      const size_t pix = (size_t)(f * H + 4 * ty + aa) * W + xx;
-      const size_t off = C8 ? (size_t)(co >> 3) * plane + pix * 8 + (co & 7) : pix * CO + co;
-      *reinterpret_cast<f32x4*>(yout + off) = o;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const f32x4 m0 = acc[r][0][nt], m1 = acc[r][1][nt], m2 = acc[r][2][nt];
+        f32x4* zp = reinterpret_cast<f32x4*>(Z + (18 + (3 * rh + r) * 4) * W4_ZS + l16 * W4_CS + 4 * q);
+        const f32x4 sm = m0 + m1, df = m0 - m1;
+        zp[0] = sm;
+        zp[W4_ZS / 4] = 2.f * df;
+        zp[2 * W4_ZS / 4] = 4.f * sm;
+        zp[3 * W4_ZS / 4] = 8.f * df + m2;
+      }
+    }
+    __syncthreads();
+    if (ulive) {
+      f32x4 P[6];
+      const int eb = ub == 3 ? 1 : ub;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const float* e = Z + (i * 3 + eb) * W4_ZS + (4 * ucq) * W4_CS + utile;
+        const float* f = Z + (18 + i * 4 + ub) * W4_ZS + (4 * ucq) * W4_CS + utile;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) P[i][c] = e[c * W4_CS] + f[c * W4_CS];
+      }
+      const int co = cob * 48 + nt * 16 + 4 * ucq;
+      const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 s12 = P[1] + P[2], d12 = P[1] - P[2], s34 = P[3] + P[4], d34 = P[3] - P[4];
+      f32x4 y[4];
+      y[0] = P[0] + s12 + s34;
+      y[1] = d12 + 2.f * d34;
+      y[2] = s12 + 4.f * s34;
+      y[3] = d12 + 8.f * d34 + P[5];
+#pragma unroll
+      for (int aa = 0; aa < 4; ++aa) {
+        if (4 * uty + aa >= H) break;  // partial tiles at the bottom edge (H % 4 != 0)
+        f32x4 o = y[aa] + bias;
+        if constexpr (RELU) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
+        }
+        const size_t pix = (size_t)(uf * H + 4 * uty + aa) * W + uxx;
+        const size_t off = C8 ? (size_t)(co >> 3) * plane + pix * 8 + (co & 7) : pix * CO + co;
+        *reinterpret_cast<f32x4*>(yout + off) = o;
+      }
     }
   }
 }
@@ -359,18 +432,18 @@ bool wino4_geometry(const ConvParams& p, W4Geo* g, int* n_blocks) {
   if (TR * TC < 12) return false;
   const int PC = 4 * TC + 2, rp0 = (PC - 1) + (PC - 1) / 4 + 1;
   // RP, SS: fewest tiles sharing a 16-B bank quad of a 256-B row (ds_read_b64: a 32-lane group = 16
-  // tiles x one channel pair), then the fewest DMA instructions
+  // tiles x one channel pair), then the 4-stage ring (<= 16 DMA instructions), then the fewest DMAs
   int best = 1 << 30;
   for (int rp = rp0; rp < rp0 + 16; ++rp)
     for (int ss = 6 * rp; ss < 6 * rp + 16; ++ss) {
       const int ni = (2 * TR * ss + 63) / 64;
-      if (ni > W4_WAVES * W4_DPW_MAX) continue;
+      if (ni > W4_WAVES * 6) continue;
       int cnt[16] = {0}, m = 0;
       for (int t = 0; t < TR * TC; ++t) {
         const int v = ((t / TC) * ss + 5 * (t % TC)) & 15;
         if (++cnt[v] > m) m = cnt[v];
       }
-      const int score = m * 1000 + ni;
+      const int score = m * 1000 + (ni <= 16 ? 0 : 100) + ni;
       if (score < best) best = score, g->RP = rp, g->SS = ss;
     }
   if (best == 1 << 30) return false;
@@ -400,18 +473,22 @@ bool wino4_supported(const ConvParams& p) {
          ((size_t)1 << 31) && wino4_geometry(p, &g, &nb);
 }
 
-// p.w: wino4_transform_weights' layout.
+// p.w: wino4_transform_weights' layout. (The launch templates are called from this non-template
+// function: instantiated from inside another template, hipcc left the kernels' host stubs undefined.)
 hipError_t launch_wino4(const ConvParams& p, hipStream_t s) {
   if (!wino4_supported(p)) return hipErrorInvalidValue;
   W4Geo g;
   int nb;
   wino4_geometry(p, &g, &nb);
+  const int dpw = (g.NI + W4_WAVES - 1) / W4_WAVES;
   switch (p.Cin >> 3) {
-    // (launch_w4 called from this non-template function: instantiated from inside another template,
-    // hipcc left the kernels' host stubs undefined)
-    case 8: return g.NI <= W4_WAVES * 3 ? launch_w4<8, 3>(p, g, nb, s) : launch_w4<8, 4>(p, g, nb, s);
-    case 16: return g.NI <= W4_WAVES * 3 ? launch_w4<16, 3>(p, g, nb, s) : launch_w4<16, 4>(p, g, nb, s);
-    default: return g.NI <= W4_WAVES * 3 ? launch_w4<0, 3>(p, g, nb, s) : launch_w4<0, 4>(p, g, nb, s);
+    case 8:
+      return dpw <= 4 ? launch_w4<8, 4>(p, g, nb, s) : dpw == 5 ? launch_w4<8, 5>(p, g, nb, s) : launch_w4<8, 6>(p, g, nb, s);
+    case 16:
+      return dpw <= 4 ? launch_w4<16, 4>(p, g, nb, s)
+                      : dpw == 5 ? launch_w4<16, 5>(p, g, nb, s) : launch_w4<16, 6>(p, g, nb, s);
+    default:
+      return dpw <= 4 ? launch_w4<0, 4>(p, g, nb, s) : dpw == 5 ? launch_w4<0, 5>(p, g, nb, s) : launch_w4<0, 6>(p, g, nb, s);
   }
 }
 
@@ -422,9 +499,10 @@ double wino4_exec_gflop(const ConvParams& p) {
   return wino4_geometry(p, &g, &nb) ? 2.0 * nb * 16.0 * 36.0 * p.Cin * 48.0 * 1e-9 : 0.0;
 }
 
-// U[cout_p/48][cin_p/8][6 i][3 nt][3 gg][64 lane][4 comp] from folded weights w[cout][cin][3][3] (double):
-// lane = k4 * 16 + n, m = 4 gg + comp = 2 j + ks; element (i, j) of G g G^T for input channel
-// chunk * 8 + 2 k4 + ks and output channel cob * 48 + nt * 16 + n.
+// U[cout_p/48][cin_p/8][4 waves][14][64 lane][4] from folded weights w[cout][cin][3][3] (double): wave
+// w = (rh, ch) = (w / 2, w % 2), lane = k4 * 16 + n, component m = 4 g + comp = ((r * 2 + ks) * 3 + nt)
+// * 3 + jj (m >= 54: zero); element (3 rh + r, 3 ch + jj) of G g G^T for input channel chunk * 8 +
+// 2 k4 + ks and output channel cob * 48 + nt * 16 + n.
 void wino4_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U) {
   static const double G[6][3] = {{1.0 / 4, 0, 0},
                                  {-1.0 / 6, -1.0 / 6, -1.0 / 6},
@@ -432,8 +510,9 @@ void wino4_transform_weights(const double* w, int cout, int cin, int cout_p, int
                                  {1.0 / 24, 1.0 / 12, 1.0 / 6},
                                  {1.0 / 24, -1.0 / 12, 1.0 / 6},
                                  {0, 0, 1}};
-  const int nch = cin_p / 8;
-  for (size_t i = 0; i < (size_t)36 * cin_p * cout_p; ++i) U[i] = 0.f;
+  const int nch = cin_p / 8, ncob = cout_p / 48;
+  const size_t total = (size_t)ncob * nch * W4_WAVES * W4_NU * 256;
+  for (size_t i = 0; i < total; ++i) U[i] = 0.f;
   for (int o = 0; o < cout; ++o)
     for (int c = 0; c < cin; ++c) {
       const double* gw = w + ((size_t)o * cin + c) * 9;
@@ -445,40 +524,49 @@ void wino4_transform_weights(const double* w, int cout, int cin, int cout_p, int
       for (int i = 0; i < 6; ++i)
         for (int j = 0; j < 6; ++j) {
           const double u = tmp[i][0] * G[j][0] + tmp[i][1] * G[j][1] + tmp[i][2] * G[j][2];
-          const int m = 2 * j + ks, gg = m / 4, comp = m % 4;
-          U[(((((((size_t)cob * nch + chunk) * 6 + i) * 3 + nt) * 3 + gg) * 64) + k4 * 16 + n) * 4 + comp] = (float)u;
+          const int wv = (i / 3) * 2 + j / 3, r = i % 3, jj = j % 3;
+          const int m = ((r * 2 + ks) * 3 + nt) * 3 + jj, gi = m / 4, comp = m % 4;
+          U[((((((size_t)cob * nch + chunk) * W4_WAVES + wv) * W4_NU + gi) * 64) + k4 * 16 + n) * 4 + comp] = (float)u;
         }
     }
 }
 
+// Floats of wino4_transform_weights' output for a cin_p x cout_p conv.
+size_t wino4_weight_floats(int cin_p, int cout_p) {
+  return (size_t)(cout_p / 48) * (cin_p / 8) * W4_WAVES * W4_NU * 256;
+}
+
 #ifdef CLASFV_KNOCKOUTS
-// tools/convbench: conv_wino4 timing knock-outs (KO bits above) on 8-chunk maps (layer1), channels-last
+// tools/convbench: conv_wino4 timing knock-outs (KO bits above) on 8- or 16-chunk maps, channels-last
 // output with ReLU.
 template <int KO>
 static hipError_t launch_w4ko(const ConvParams& p, const W4Geo& g, int nb, hipStream_t s) {
   if (p.Cin == 128)
-    hipLaunchKernelGGL((conv_wino4<16, false, true, 3, KO>), dim3(nb), dim3(W4_THREADS), 0, s, p, g);
+    hipLaunchKernelGGL((conv_wino4<16, false, true, 4, KO>), dim3(nb), dim3(W4_THREADS), 0, s, p, g);
   else
-    hipLaunchKernelGGL((conv_wino4<8, false, true, 3, KO>), dim3(nb), dim3(W4_THREADS), 0, s, p, g);
+    hipLaunchKernelGGL((conv_wino4<8, false, true, 4, KO>), dim3(nb), dim3(W4_THREADS), 0, s, p, g);
   return hipGetLastError();
 }
 hipError_t launch_wino4_ko(const ConvParams& p, hipStream_t s, int ko) {
   W4Geo g;
   int nb;
-  if (!wino4_supported(p) || (p.Cin != 64 && p.Cin != 128) || p.y_c8 || !p.relu || !wino4_geometry(p, &g, &nb) || g.NI > 18)
+  if (!wino4_supported(p) || (p.Cin != 64 && p.Cin != 128) || p.y_c8 || !p.relu || !wino4_geometry(p, &g, &nb) ||
+      g.NI > 16)
     return hipErrorInvalidValue;
   switch (ko) {
-    case 0: return launch_w4ko<0>(p, g, nb, s);
     case 1: return launch_w4ko<1>(p, g, nb, s);
     case 2: return launch_w4ko<2>(p, g, nb, s);
     case 3: return launch_w4ko<3>(p, g, nb, s);
     case 4: return launch_w4ko<4>(p, g, nb, s);
     case 8: return launch_w4ko<8>(p, g, nb, s);
     case 15: return launch_w4ko<15>(p, g, nb, s);
-    case 16: return launch_w4ko<16>(p, g, nb, s);
     case 32: return launch_w4ko<32>(p, g, nb, s);
     case 47: return launch_w4ko<47>(p, g, nb, s);
-    default: return hipErrorInvalidValue;
+    case 64: return launch_w4ko<64>(p, g, nb, s);
+    case 128: return launch_w4ko<128>(p, g, nb, s);
+    case 192: return launch_w4ko<192>(p, g, nb, s);
+    case 256: return launch_w4ko<256>(p, g, nb, s);
+    default: return launch_w4ko<0>(p, g, nb, s);
   }
 }
 #endif

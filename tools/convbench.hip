@@ -112,7 +112,7 @@ int main(int argc, char** argv) {
   p.relu = 1;
   const size_t nx = (size_t)N * T * H * W * Cin, ny = (size_t)p.M * Cout;
   p.x = bf ? to_bf16_dev(nx, 0.f, 1.f, 1) : dev_random(nx, 0.f, 1.f, 1);
-  const size_t nw = wino4 ? (size_t)36 * Cin * Cout : winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
+  const size_t nw = wino4 ? (size_t)(Cout / 48) * (Cin / 8) * 14336 : winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
   p.w = bf ? to_bf16_dev(nw, -0.05f, 0.05f, 2) : dev_random(nw, -0.05f, 0.05f, 2);
   p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
   p.res = (getenv("CB_NORES") || wino4) ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
