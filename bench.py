@@ -176,8 +176,10 @@ def kernel_roofline(ktimes, peak, dtype):
             "algorithmic_gflop_per_launch": round(k["gflop"] / n, 3),
             "algorithmic_equiv_tflops": round(k["gflop"] / max(k["ms"], 1e-9), 3),
             "traffic_source": tr and tr["source"],
-            "note": "achieved = MFMA work issued (Winograd F(2x2,3x3): 16 of the 36 direct products per 2x2 "
-                    "tile; F(4,3): 6 of 12 per 4 frames; padded channels and partial tiles counted) / time"}
+            "note": "achieved = MFMA work issued (Winograd F(4x4,3x3): 36 of the 144 direct products per 4x4 "
+                    "tile, 16-tile MFMA groups; F(2x2,3x3): 16 of 36 per 2x2 tile; F(4,3): 6 of 12 per 4 frames; "
+                    "padded channels and partial tiles counted) / time; algorithmic_equiv_tflops = the direct-"
+                    "convolution FLOPs of the same launches / time"}
 
 
 def profiled_traffic(kernel, dtype):

@@ -118,7 +118,7 @@ __device__ inline void bt_cols(const f32x2 (&t)[6], f32x2 (&v)[3]) {
 // NCH: input-channel chunks (8 channels each; 0 = runtime). C8: 8-channel-blocked output. DPW: DMA
 // instructions per wave per chunk (W4Ring). KO: timing knock-outs for tools/convbench (0 in the product;
 // results are wrong otherwise): 1 no transform reads / VALU, 2 no U reloads, 4 no epilogue, 8 no DMAs
-// in the chunk loop, 32 no chunk barrier; 64 n: the first round's second blocks sleep n x 8128 cycles.
+// in the chunk loop, 16 no transform reads (its VALU kept), 32 no chunk barrier; 64 n: the first round's second blocks sleep n x 8128 cycles.
 template <int NCH, bool C8, bool RELU, int DPW, int KO = 0>
 __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wino4(ConvParams p,
                                                                                                      W4Geo g) {
@@ -201,7 +201,12 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         const int co = (c + (c >> 2)) * 16;  // pixel columns 0..5 of the window -> slots 0,1,2,3,5,6
         f32x2 e[5];
 #pragma unroll
-        for (int q = 0; q < 5; ++q) e[q] = *reinterpret_cast<const f32x2*>(base + q * rp16 + co);
+        for (int q = 0; q < 5; ++q) {
+          if constexpr ((KO & 16) != 0)  // probe: the transform's VALU without its LDS reads
+            e[q] = f32x2{(float)(lane + q + c + stage), (float)(lane * q - c)};
+          else
+            e[q] = *reinterpret_cast<const f32x2*>(base + q * rp16 + co);
+        }
         f32x2 t3[3];
         bt_rows<RH>(e, t3);
 #pragma unroll
@@ -562,6 +567,7 @@ hipError_t launch_wino4_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 15: return launch_w4ko<15>(p, g, nb, s);
     case 32: return launch_w4ko<32>(p, g, nb, s);
     case 47: return launch_w4ko<47>(p, g, nb, s);
+    case 16: return launch_w4ko<16>(p, g, nb, s);
     case 64: return launch_w4ko<64>(p, g, nb, s);
     case 128: return launch_w4ko<128>(p, g, nb, s);
     case 192: return launch_w4ko<192>(p, g, nb, s);
