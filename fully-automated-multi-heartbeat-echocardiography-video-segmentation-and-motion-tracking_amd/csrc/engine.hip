@@ -170,6 +170,11 @@ struct clasfv_engine {
   char* arena = nullptr;
   size_t arena_bytes = 0;
   float* zero = nullptr;  // 256 zero bytes for padding taps
+  // side stream of clasfv_forward: the decoder projections of the stem/layer1, layer2 and layer3 taps
+  // run there as soon as their tap exists, filling the CUs the backbone's later (small-grid) convs
+  // leave idle; the decoder waits for them (events, no host synchronisation)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // per-kernel HIP-event timing of clasfv_forward (clasfv_set_kernel_timing)
   bool ktime = false;
   std::vector<hipEvent_t> evs;  // event pool; evs[0..nev) recorded since the last read
@@ -567,6 +572,9 @@ int clasfv_destroy(clasfv_t h) {
     (void)hipFree(c.dws16);
   }
   for (auto& c : h->proj) (void)hipFree(c.dw);
+  if (h->side) (void)hipStreamDestroy(h->side);
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   (void)hipFree(h->b1);
   (void)hipFree(h->w2);
   (void)hipFree(h->b2);
@@ -792,6 +800,25 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   };
   // scratch for a temporal conv reading MID: the rest of MID past its input
   const size_t mid_bytes = L.off[MID + 1] - L.off[MID];
+  if (!h->side) {
+    HIP_TRY(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+  }
+  // a decoder projection on the side stream once its tap is complete on s (timed with its own events)
+  auto run_side = [&](const Conv& c, const void* xin, const Shape5& in, void* y, Shape5& out, const void* x2) {
+    HIP_TRY(hipEventRecord(h->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    const int e0 = h->ktime ? tick(h, h->side) : -1;
+    const char* kname = "";
+    int rc_ = run_conv(c, xin, in, y, out, nullptr, false, h->side, h->zero, x2, &kname, h->tune);
+    if (!rc_ && e0 >= 0) {
+      const int e1 = tick(h, h->side);
+      if (e1 >= 0) h->recs.push_back({kname, conv_gflop(c, out), conv_exec_gflop(c, out, kname), e0, e1});
+    }
+    if (!rc_) HIP_TRY(hipEventRecord(h->ev_join, h->side));
+    return rc_;
+  };
   auto run = [&](const Conv& c, const void* xin, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
                  const void* x2 = nullptr, int x_c8 = 0, int y_c8 = 0) {
     const char* kname = "";
@@ -813,6 +840,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   HIP_TRY(launch_pack_input(x, reinterpret_cast<float*>(buf(XIN)), N, T, H * W, s));
   timed("pack_input_kernel", 0.0, 0.0);
   Shape5 sx{N, T, H, W, 4}, s0, sx0;
+  Shape5 sp, sp2, sp3, sp4;  // decoder tap projections
   int rc;
   size_t ci = 0;
   // Conv2Plus1D mid tensors (and the stem's) are 8-channel-blocked where c8_pair allows
@@ -850,14 +878,18 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
     }
     taps[li + 1] = cur;
     taps_shape[li + 1] = cs;
+    // decoder projections at tap resolution (P01 = W0 f0 + W1 f1, P2, P3) on the side stream while
+    // layer4 runs: its convs (600-920 blocks for 30 clips, 1.2-1.8 rounds of the chip's block slots)
+    // leave CUs idle that the projections fill (forked earlier, P01 only shared layer2's full grids:
+    // r03i trace, no gain); P4 after layer4 on s
+    if (li == 2) {
+      if ((rc = run_side(h->proj[0], taps[0], taps_shape[0], buf(P01), sp, taps[1]))) return rc;
+      if ((rc = run_side(h->proj[2], taps[2], taps_shape[2], buf(PP2), sp2, nullptr))) return rc;
+      if ((rc = run_side(h->proj[3], taps[3], taps_shape[3], buf(PP3), sp3, nullptr))) return rc;
+    }
   }
-  // decoder projections at tap resolution: P01 = W0 f0 + W1 f1, P2..P4
-  Shape5 sp;
-  if ((rc = run(h->proj[0], taps[0], taps_shape[0], buf(P01), sp, nullptr, false, taps[1]))) return rc;
-  Shape5 sp2, sp3, sp4;
-  if ((rc = run(h->proj[2], taps[2], taps_shape[2], buf(PP2), sp2, nullptr, false))) return rc;
-  if ((rc = run(h->proj[3], taps[3], taps_shape[3], buf(PP3), sp3, nullptr, false))) return rc;
   if ((rc = run(h->proj[4], taps[4], taps_shape[4], buf(PP4), sp4, nullptr, false))) return rc;
+  HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));  // the side stream's projections are complete
 
   DecParams d{};
   const Shape5 tsh[4] = {sp, sp2, sp3, sp4};

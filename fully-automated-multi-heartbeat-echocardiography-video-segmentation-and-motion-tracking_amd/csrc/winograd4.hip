@@ -245,7 +245,11 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
 
   if constexpr ((KO & 64) != 0) {  // stagger probe: the second block of each CU in the first round starts late
     if (blockIdx.x >= 256 && blockIdx.x < 512)
-      for (int i = 0; i < KO / 64; ++i) __builtin_amdgcn_s_sleep(127);
+      for (int i = 0; i < (KO & 4095) / 64; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+  if constexpr ((KO & 4096) != 0) {  // the same with the odd blocks of the first round
+    if ((blockIdx.x & 1) && blockIdx.x < 512)
+      for (int i = 0; i < 2; ++i) __builtin_amdgcn_s_sleep(127);
   }
   // ---- prologue: raw(0), raw(1) and U(0) in flight. Per chunk every wave then issues exactly DPW
   // DMAs + 14 U loads (past-the-end ones re-read chunk 0), so the counted vmcnt waits are exact.
@@ -572,6 +576,7 @@ hipError_t launch_wino4_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 128: return launch_w4ko<128>(p, g, nb, s);
     case 192: return launch_w4ko<192>(p, g, nb, s);
     case 256: return launch_w4ko<256>(p, g, nb, s);
+    case 4096: return launch_w4ko<4096>(p, g, nb, s);
     default: return launch_w4ko<0>(p, g, nb, s);
   }
 }

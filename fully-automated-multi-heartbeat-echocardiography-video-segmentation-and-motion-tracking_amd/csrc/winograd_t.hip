@@ -368,11 +368,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   issue(k0, 0);
   __builtin_amdgcn_sched_barrier(0);
   for (int k = k0; k < k1; ++k) {
-    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): chunk k's DMAs (own) landed
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();        // everyone's landed; everyone done with the other stage
-    __builtin_amdgcn_sched_barrier(0);
-    if (k + 1 < k1) issue(k + 1, (k + 1 - k0) & 1);
+    // (EPI >= 256: convbench timing knock-outs, results wrong: 256 no transform VALU, 512 no DMAs in
+    // the loop, 1024 no epilogue, 2048 no wait / barrier)
+    if constexpr ((EPI & 2048) == 0) {
+      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): chunk k's DMAs (own) landed
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();        // everyone's landed; everyone done with the other stage
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr ((EPI & 512) == 0)
+      if (k + 1 < k1) issue(k + 1, (k + 1 - k0) & 1);
     __builtin_amdgcn_sched_barrier(0);
     const float* st = reinterpret_cast<const float*>(smem + ((k - k0) & 1) * G::STAGE);
     // frames of tile m: d[4m .. 4m + 5] (in time), or d[6m .. 6m + 5] (COLS: the m-th column group)
@@ -390,6 +395,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if constexpr (COLS) d[5] = f32x2{0.f, 0.f};
     }
     f32x2 v[2][6];
+    if constexpr ((EPI & 256) != 0) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int e = 0; e < 6; ++e) v[m][e] = d[MS * m + e];
+    } else
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -419,6 +430,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
   }
 
+  if constexpr ((EPI & 1024) != 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < 6; ++e)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) sum += acc[e][m][nt][0] + acc[e][m][nt][1] + acc[e][m][nt][2] + acc[e][m][nt][3];
+    if (sum == 1234.5f) reinterpret_cast<float*>(p.y)[tid] = sum;
+    return;
+  }
   // epilogue: y = A^T M in registers, 16-B bias / residual loads and stores
   const float* res = reinterpret_cast<const float*>(p.res);
   float* yout = SPLIT ? p.part + (size_t)split * ((size_t)p.N * T * HW * CO) : reinterpret_cast<float*>(p.y);
@@ -587,6 +609,13 @@ hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko) {
       return hipGetLastError();
     }
     case 500: return p.x_c8 && !winot_c8_ok(p) ? hipErrorInvalidValue : winot5_dispatch(p, s);
+    // knock-outs (TS = 4, NT = 4, EPI 2 + bits): 801 no transform, 802 no loop DMAs, 804 no epilogue,
+    // 808 no wait / barrier, 815 all
+    case 801: return winot5_launch_e<4, 4, 2 + 256>(p, s);
+    case 802: return winot5_launch_e<4, 4, 2 + 512>(p, s);
+    case 804: return winot5_launch_e<4, 4, 2 + 1024>(p, s);
+    case 808: return winot5_launch_e<4, 4, 2 + 2048>(p, s);
+    case 815: return winot5_launch_e<4, 4, 2 + 256 + 512 + 1024 + 2048>(p, s);
     case 502: return winot5_dispatch(p, s, 2);
     case 504: return winot5_dispatch(p, s, 4);
   }

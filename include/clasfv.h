@@ -56,7 +56,8 @@ enum { CLASFV_FUSE_MAJORITY = 0, CLASFV_FUSE_SIMPLE = 1, CLASFV_FUSE_STAPLE = 2,
 enum { CLASFV_DTYPE_FP32 = 0, CLASFV_DTYPE_BF16 = 1 };
 
 /* Kernel-variant switches (A/B testing against the kernels each product kernel replaced; every
- * variant computes the same function -- NO_SPLIT_K the same sums in another fp32 summation order).
+ * variant computes the same function -- NO_SPLIT_K the same sums in another fp32 summation order,
+ * NO_WINO4 the same convolutions through F(2x2,3x3) instead of F(4x4,3x3) fp32 rounding).
  * Read once, at clasfv_create, from the environment variable named in the comment (set = on), or set
  * with clasfv_set_kernel_variants. */
 enum {
