@@ -68,6 +68,8 @@ struct DecParams {
   DecTap tap[4];      // (stem+layer1), layer2, layer3, layer4
   const float* b1;    // [64]    comb_1 bias with BN1 folded
   const float* w2;    // [64*64] comb_2 weight with BN2 folded, [n][k]
+  const void* w2x3;   // fp32 engines: W2 as three bf16 pieces (hi, mid, lo: w2 = hi + mid + lo to 24
+                      // bits) in the MFMA lane order [3][nt 4][kb 2][l16 16][q 4][8], see decoder.hip
   const float* b2;    // [64]
   const float* wh;    // [8*64]  rows: seg0, seg1, mot0..mot3, 0, 0
   const float* bh;    // [8]
@@ -75,6 +77,7 @@ struct DecParams {
   float* mot;         // (N,4,T,H,W)
   int N, T, H, W;
   int bf16;           // comb_2 on bf16 MFMAs (bf16 engines; taps, heads and outputs stay fp32)
+  int x3;             // fp32 engines: comb_2 as six bf16 products of 3-way split operands (fp32-accurate)
 };
 
 // Launchers (stream-ordered, no synchronisation). Return hipError_t of the launch.

@@ -96,25 +96,62 @@ __device__ inline void split_bf16x8(f32x4 a, f32x4 b, bf16x8& hi, bf16x8& lo) {
   lo = to_bf16x8(ra, rb);
 }
 
+// x = hi + mid + lo, each a bf16 of the remainder (round to nearest): 24 mantissa bits, fp32's
+__device__ inline void split3_bf16x8(f32x4 a, f32x4 b, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+  hi = to_bf16x8(a, b);
+  f32x4 ra, rb;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    ra[e] = a[e] - (float)hi[e];
+    rb[e] = b[e] - (float)hi[4 + e];
+  }
+  mid = to_bf16x8(ra, rb);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    ra[e] -= (float)mid[e];
+    rb[e] -= (float)mid[4 + e];
+  }
+  lo = to_bf16x8(ra, rb);
+}
+
 // Steps 3-5 of the bf16-engine decoder (see decoder_kernel): h1[mt][c][j] = channel 16c + 4q + j of
 // voxel (row h0 + 2 wid + mt, column w0 + l16). comb_2 runs as three bf16 products per K block
 // (hi.hi + hi.lo + lo.hi of the split operands: ~fp32 accuracy at 6 instead of 32 MFMA slots).
+// X3 (fp32 engines): comb_2 as six bf16 products of 3-way split operands (lo.hi + hi.lo + mid.mid +
+// mid.hi + hi.mid + hi.hi, smallest first; the dropped terms are below 2^-24 of the product) with fp32
+// accumulation -- fp32-accurate, on the bf16 matrix rate (12 instead of 32 MFMA slots; on gfx950 the
+// f32 MFMA shares the f32 vector rate with the interpolation, which the bf16 MFMA does not). W2's
+// pieces come split on the host (DecParams::w2x3), h1's are split here.
+template <bool X3>
 __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[2][4], int t, int n, int h0, int w0,
                                           int wid, int q, int l16) {
-  bf16x8 hh[2][2], hl[2][2];
+  bf16x8 hh[2][2], hl[2][2], hm[2][2];
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) split_bf16x8(h1[mt][2 * kb], h1[mt][2 * kb + 1], hh[mt][kb], hl[mt][kb]);
+    for (int kb = 0; kb < 2; ++kb) {
+      if constexpr (X3)
+        split3_bf16x8(h1[mt][2 * kb], h1[mt][2 * kb + 1], hh[mt][kb], hm[mt][kb], hl[mt][kb]);
+      else
+        split_bf16x8(h1[mt][2 * kb], h1[mt][2 * kb + 1], hh[mt][kb], hl[mt][kb]);
+    }
   f32x4 acc[2][4];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     const float* wr = p.w2 + (16 * nt + l16) * 64 + 4 * q;
-    bf16x8 wh_[2], wl_[2];
+    bf16x8 wh_[2], wl_[2], wm_[2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-      split_bf16x8(*reinterpret_cast<const f32x4*>(wr + 32 * kb), *reinterpret_cast<const f32x4*>(wr + 32 * kb + 16),
-                   wh_[kb], wl_[kb]);
+    for (int kb = 0; kb < 2; ++kb) {
+      if constexpr (X3) {
+        const bf16x8* w3 = reinterpret_cast<const bf16x8*>(p.w2x3) + ((nt * 2 + kb) * 16 + l16) * 4 + q;
+        wh_[kb] = w3[0];
+        wm_[kb] = w3[512];
+        wl_[kb] = w3[1024];
+      } else {
+        split_bf16x8(*reinterpret_cast<const f32x4*>(wr + 32 * kb), *reinterpret_cast<const f32x4*>(wr + 32 * kb + 16),
+                     wh_[kb], wl_[kb]);
+      }
+    }
     const f32x4 bb = *reinterpret_cast<const f32x4*>(p.b2 + 16 * nt + 4 * q);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -123,6 +160,11 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
       for (int kb = 0; kb < 2; ++kb) {
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl_[kb], hh[mt][kb], a, 0, 0, 0);
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh_[kb], hl[mt][kb], a, 0, 0, 0);
+        if constexpr (X3) {
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm_[kb], hm[mt][kb], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm_[kb], hh[mt][kb], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh_[kb], hm[mt][kb], a, 0, 0, 0);
+        }
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh_[kb], hh[mt][kb], a, 0, 0, 0);
       }
 #pragma unroll
@@ -176,11 +218,12 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
 // BF = 1 (BASELINE config[4]): comb_2 on v_mfma_f32_16x16x32_bf16 with split (hi + lo) bf16 h1 and W2
 // (one 32-deep K block = the 8 channels 16c + 4q + j, c in {2kb, 2kb+1}, that lane group q already
 // holds, so both operands keep the fp32 path's register layout), fp32 accumulation; fp32 heads.
-// MODE: 0 = fp32, 1 = bf16 comb_2; timing knock-outs for tools/convbench.hip (CLASFV_KNOCKOUTS builds
-// only; wrong results): 2 = no comb_2 / head MFMAs, 3 = no interpolation.
+// MODE: 0 = fp32 (v_mfma_f32_16x16x4_f32 comb_2), 1 = bf16 comb_2, 4 = fp32-accurate comb_2 on six
+// split-bf16 products (the fp32 engines' default); timing knock-outs for tools/convbench.hip
+// (CLASFV_KNOCKOUTS builds only; wrong results): 2 = no comb_2 / head MFMAs, 3 = no interpolation.
 template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void decoder_kernel(DecParams p) {
-  constexpr int BF = MODE == 1;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ? 4 : 5, MODE == 4 ? 4 : 5))) void decoder_kernel(DecParams p) {
+  constexpr int BF = MODE == 1 || MODE == 4;
   extern __shared__ __align__(16) float smem[];
   float* stage = smem;  // STAGE_FLOATS
 
@@ -340,7 +383,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
       for (int j = 0; j < 4; ++j) h1[mt][c][j] = fmaxf(h1[mt][c][j], 0.f);
 
   if constexpr (BF) {
-    decoder_heads_bf16(p, h1, t, n, h0, w0, wid, q, l16);
+    decoder_heads_bf16<MODE == 4>(p, h1, t, n, h0, w0, wid, q, l16);
     return;
   }
   // 3. h2^T[n][v] = sum_k W2[n][k] h1[v][k]; MFMA j of lane group q covers k = 16c + 4q + j
@@ -436,7 +479,7 @@ static hipError_t launch_dec(const DecParams& p, hipStream_t s, int mode) {
   if (nb >= ((size_t)1 << 31)) return hipErrorInvalidValue;
   constexpr size_t lds = (size_t)STAGE_FLOATS * 4;
   static_assert(lds <= 64 * 1024, "default dynamic LDS limit");
-  void (*k)(DecParams) = mode == 1 ? decoder_kernel<1> : decoder_kernel<0>;
+  void (*k)(DecParams) = mode == 1 ? decoder_kernel<1> : mode == 4 ? decoder_kernel<4> : decoder_kernel<0>;
 #ifdef CLASFV_KNOCKOUTS
   if (mode == 2) k = decoder_kernel<2>;
   if (mode == 3) k = decoder_kernel<3>;
@@ -445,11 +488,14 @@ static hipError_t launch_dec(const DecParams& p, hipStream_t s, int mode) {
   return hipGetLastError();
 }
 
-hipError_t launch_decoder(const DecParams& p, hipStream_t s) { return launch_dec(p, s, p.bf16 ? 1 : 0); }
+hipError_t launch_decoder(const DecParams& p, hipStream_t s) {
+  if (p.x3 && !p.w2x3) return hipErrorInvalidValue;
+  return launch_dec(p, s, p.bf16 ? 1 : p.x3 ? 4 : 0);
+}
 
 #ifdef CLASFV_KNOCKOUTS
 // tools/convbench.hip: ko 0 = product; 2, 3 = decoder_kernel's knock-out modes
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko) {
-  return launch_dec(p, s, ko == 2 || ko == 3 ? ko : (p.bf16 ? 1 : 0));
+  return launch_dec(p, s, ko == 2 || ko == 3 ? ko : (p.bf16 ? 1 : p.x3 ? 4 : 0));
 }
 #endif

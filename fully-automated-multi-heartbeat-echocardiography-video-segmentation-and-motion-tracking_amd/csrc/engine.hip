@@ -113,6 +113,7 @@ int env_variants() {
   if (ts1 && ts1[0] == '0') f |= CLASFV_VARIANT_WINOT_NO_TS1;
   if (on("CLASFV_NO_SPLIT_K")) f |= CLASFV_VARIANT_NO_SPLIT_K;
   if (on("CLASFV_NO_WINO4")) f |= CLASFV_VARIANT_NO_WINO4;
+  if (on("CLASFV_NO_DECODER_X3")) f |= CLASFV_VARIANT_NO_DECODER_X3;
   return f;
 }
 
@@ -163,6 +164,7 @@ struct clasfv_engine {
   std::vector<Conv> convs;  // backbone, execution order
   Conv proj[5];             // decoder projections (stem, layer1..4) -> 64 channels
   float *b1 = nullptr, *w2 = nullptr, *b2 = nullptr, *wh = nullptr, *bh = nullptr;
+  void* w2x3 = nullptr;  // W2 as three bf16 pieces in the decoder's MFMA lane order (fp32 engines)
   bool ready = false;
   int dtype = CLASFV_DTYPE_FP32;  // compute dtype of the encoder convs
   Tuning tune;                    // kernel variants / tile overrides (environment at create)
@@ -577,6 +579,7 @@ int clasfv_destroy(clasfv_t h) {
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   (void)hipFree(h->b1);
   (void)hipFree(h->w2);
+  (void)hipFree(h->w2x3);
   (void)hipFree(h->b2);
   (void)hipFree(h->wh);
   (void)hipFree(h->bh);
@@ -731,8 +734,31 @@ int clasfv_finalize(clasfv_t h) {
     (void)hipFree(*d);
     *d = nullptr;
   }
+  // W2 = hi + mid + lo, each piece the bf16 of the remainder (exact in double), in the lane order of the
+  // decoder's comb_2 B operand: [piece][nt][kb][l16][q][e], element e of lane (l16, q) = W2[16nt + l16]
+  // [32kb + 4q + (e < 4 ? e : 12 + e)] (decoder.hip, decoder_heads_bf16<true>)
+  std::vector<float> w2x3(3 * 64 * 64);
+  for (int nt = 0; nt < 4; ++nt)
+    for (int kb = 0; kb < 2; ++kb)
+      for (int l = 0; l < 16; ++l)
+        for (int q = 0; q < 4; ++q)
+          for (int e = 0; e < 8; ++e) {
+            const size_t i = ((((size_t)nt * 2 + kb) * 16 + l) * 4 + q) * 8 + e;
+            double r = w2f[(16 * nt + l) * 64 + 32 * kb + 4 * q + (e < 4 ? e : 12 + e)];
+            for (int pc = 0; pc < 3; ++pc) {
+              const uint16_t b = to_bf16((float)r);
+              uint32_t u = (uint32_t)b << 16;
+              float f;
+              memcpy(&f, &u, 4);
+              w2x3[(size_t)pc * 4096 + i] = f;
+              r -= f;
+            }
+          }
+  (void)hipFree(h->w2x3);
+  h->w2x3 = nullptr;
   int rc = upload(b1, &h->b1);
   if (!rc) rc = upload(w2f, &h->w2);
+  if (!rc) rc = upload_bf16(w2x3, &h->w2x3);
   if (!rc) rc = upload(b2, &h->b2);
   if (!rc) rc = upload(whf, &h->wh);
   if (!rc) rc = upload(bhf, &h->bh);
@@ -762,7 +788,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0x3FF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~0x7FF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;
@@ -912,11 +938,13 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   d.mot = mot;
   d.N = N, d.T = T, d.H = H, d.W = W;
   d.bf16 = h->dtype == CLASFV_DTYPE_BF16 && !(h->tune.vflags & CLASFV_VARIANT_NO_DECODER_BF16);
+  d.w2x3 = h->w2x3;
+  d.x3 = h->dtype != CLASFV_DTYPE_BF16 && !(h->tune.vflags & CLASFV_VARIANT_NO_DECODER_X3);
   HIP_TRY(launch_decoder(d, s));
-  // comb_2 (64x64; three split-bf16 products in bf16 engines) and the heads (6 useful of the 16 rows
-  // of their MFMA tile) per output voxel
+  // comb_2 (64x64; three split-bf16 products in bf16 engines, six in fp32 ones) and the heads (6
+  // useful of the 16 rows of their MFMA tile) per output voxel
   timed("decoder_kernel", 2.0 * N * (double)T * H * W * (64 * 64 + 64 * 6) * 1e-9,
-        2.0 * N * (double)T * H * W * ((d.bf16 ? 3 : 1) * 64 * 64 + 64 * 16) * 1e-9);
+        2.0 * N * (double)T * H * W * ((d.bf16 ? 3 : d.x3 ? 6 : 1) * 64 * 64 + 64 * 16) * 1e-9);
   return CLASFV_OK;
 }
 

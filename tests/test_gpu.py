@@ -581,6 +581,22 @@ def test_wino4_matches_wino2(model, shape):
     assert np.all(np.abs(d[flips]) <= 2 * SEG_ATOL)
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 8, 32, 48)])
+def test_decoder_x3_matches_fp32_mfma(model, shape):
+    """The fp32 engines' comb_2 on six split-bf16 products (hi/mid/lo pieces of both operands, fp32
+    accumulation) against the fp32 MFMA comb_2 (variant no_decoder_x3): the same 64x64 product to
+    fp32 rounding, so the outputs differ only at the accumulation-order level."""
+    rng = np.random.default_rng(43)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    s3, m3 = model(x)
+    model.set_kernel_variants("no_decoder_x3")
+    s1, m1 = model(x)
+    model.set_kernel_variants()
+    assert not torch.equal(s3, s1)  # the split-bf16 comb_2 really ran
+    np.testing.assert_allclose(s3.cpu().numpy(), s1.cpu().numpy(), rtol=0, atol=SEG_ATOL / 10)
+    np.testing.assert_allclose(m3.cpu().numpy(), m1.cpu().numpy(), rtol=0, atol=MOT_ATOL / 10)
+
+
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (1, 3, 8, 32, 48)])
 def test_c8_blocked_mid_bitexact(model, shape):
     """The 8-channel-blocked mid tensors (stem and Conv2Plus1D spatial -> temporal Winograd) only
