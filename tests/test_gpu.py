@@ -594,7 +594,7 @@ def test_decoder_x3_matches_fp32_mfma(model, shape):
     model.set_kernel_variants()
     assert not torch.equal(s3, s1)  # the split-bf16 comb_2 really ran
     np.testing.assert_allclose(s3.cpu().numpy(), s1.cpu().numpy(), rtol=0, atol=SEG_ATOL / 10)
-    np.testing.assert_allclose(m3.cpu().numpy(), m1.cpu().numpy(), rtol=0, atol=MOT_ATOL / 10)
+    np.testing.assert_allclose(m3.cpu().numpy(), m1.cpu().numpy(), rtol=0, atol=MOT_ATOL / 4)
 
 
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (1, 3, 8, 32, 48)])
