@@ -111,6 +111,12 @@ bool winot_c8_ok(const ConvParams& p);
 hipError_t launch_split_sum(const ConvParams& p, hipStream_t s);
 // Split-K factor for launch_conv's conv_dma with M tile mt (1: no split; per-clip shape only).
 int dma_split_for(const ConvParams& p, int mt);
+// conv_dma_x3: fp32 implicit GEMM on split-bf16 MFMAs (six products, fp32-accurate; conv.hip)
+bool dma_x3_supported(const ConvParams& p);
+int dma_x3_bn(int cout_p);
+hipError_t launch_dma_x3(const ConvParams& p, int bn, hipStream_t s);
+void dma_x3_weight_image(const float* w, int cout_alloc, int Kp, uint16_t* out);
+size_t dma_x3_weight_elems(int cout_alloc, int Kp);
 // Split-K factor (ConvParams::n_split) for launch_winot (1: no split; per-clip shape only); the
 // caller provides ConvParams::part with n_split * M * Cout floats.
 int winot_split_for(const ConvParams& p);

@@ -24,12 +24,35 @@
 //    accumulation order: bit-identical to the untransposed form).
 #include <hip/hip_bf16.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
+
+__device__ inline bf16x8 pack_bf16x8(f32x4 a, f32x4 b) {
+  return bf16x8{(__bf16)a[0], (__bf16)a[1], (__bf16)a[2], (__bf16)a[3],
+                (__bf16)b[0], (__bf16)b[1], (__bf16)b[2], (__bf16)b[3]};
+}
+
+// x = hi + mid + lo, each the bf16 (round to nearest) of the remainder: fp32's 24 bits in 3 pieces
+__device__ inline void split3_bf16x8(f32x4 a, f32x4 b, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+  hi = pack_bf16x8(a, b);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] -= (float)hi[e];
+    b[e] -= (float)hi[4 + e];
+  }
+  mid = pack_bf16x8(a, b);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    a[e] -= (float)mid[e];
+    b[e] -= (float)mid[4 + e];
+  }
+  lo = pack_bf16x8(a, b);
+}
 
 __device__ inline int xcd_swizzle(int b, int nb) {
   const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
@@ -289,6 +312,194 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
 }
 
 // ---------------------------------------------------------------------------------------------
+// conv_dma_x3: the fp32 implicit GEMM on v_mfma_f32_16x16x32_bf16 with 3-way split operands.
+// x = hi + mid + lo (each the bf16 of the remainder: fp32's 24 bits); the product is accumulated in
+// fp32 as lo.hi + hi.lo + mid.mid + mid.hi + hi.mid + hi.hi (smallest first; the dropped terms are
+// below 2^-24 of the product), i.e. fp32-accurate, at 6 x 16 instead of 8 x 32 MFMA cycles per
+// 32-deep K block (2.67x the fp32 MFMA rate). The weights are split on the host into a bf16 image
+// [Cout_alloc][Kp/32][3 pieces][32] (dma_x3_weight_image); the activations are LDS-DMA'd as fp32
+// exactly as in conv_dma and split in registers.
+//
+// A ring stage holds one K pair = two 16-channel steps: A as two fp32 tiles of conv_dma's layout
+// (64-B rows, swizzled slots), B as 3 pieces x BN rows of 64 B (32 bf16: slot q holds, for lane group
+// q, k = 4q..4q+3 of the first step and of the second), so lane (l16, q) builds its 8-element bf16
+// operands from its f32x4 slot of each step -- the same k set on both sides of the product.
+template <int MT, int NT, int S>
+__global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, DmaDivs dv) {
+  constexpr int BM = 64 * MT, BN = 16 * NT;
+  constexpr int A_INS = BM / 16, B_INS = 3 * NT;     // DMA instructions (16 rows x 64 B) per step / pair
+  constexpr int A_PER = A_INS / 4, B_PER = (B_INS + 3) / 4;
+  constexpr int PER_WAVE = 2 * A_PER + B_PER;
+  static_assert(A_INS % 4 == 0, "A rows split evenly over the 4 waves");
+  constexpr int A_BYTES = A_INS * 1024;
+  constexpr int STAGE = (2 * A_INS + B_INS) * 1024;
+  constexpr int JUNK = S * STAGE;
+  __shared__ __align__(16) char smem[S * STAGE + 1024];
+
+  const float* x = reinterpret_cast<const float*>(p.x);
+  const float* x2 = reinterpret_cast<const float*>(p.x2);
+  const __bf16* w = reinterpret_cast<const __bf16*>(p.w);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n_split = p.n_split > 1 ? p.n_split : 1;
+  int tile = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int n_tb = gridDim.x / n_split;
+  const int split = tile / n_tb;
+  tile -= split * n_tb;
+  const int tq = fdiv(tile, dv.nt);
+  const int m0 = tq * BM, n0 = (tile - tq * n_tiles) * BN;
+  const int q = lane >> 4, l16 = lane & 15;
+  constexpr int G[4] = {0, 2, 3, 1};
+
+  const int nsteps = p.Kp / 16;           // 16-channel K steps
+  const int npairs = (nsteps + 1) / 2;    // ring stages; an odd last step pairs with zeros
+  const int drow = lane >> 2;
+  const int dq = (lane & 3) ^ G[(drow >> 2) & 3];
+  int d_t[A_PER], d_h[A_PER], d_w[A_PER], d_pix[A_PER];
+#pragma unroll
+  for (int j = 0; j < A_PER; ++j) {
+    int m = m0 + (wid * A_PER + j) * 16 + drow;
+    const bool ok = m < p.M;
+    if (!ok) m = 0;
+    const int mw = fdiv(m, dv.wo), wo = m - mw * p.Wo;
+    const int mh = fdiv(mw, dv.ho), ho = mw - mh * p.Ho;
+    const int mt = fdiv(mh, dv.to), to = mh - mt * p.To;
+    d_t[j] = ok ? to * p.st - p.pt : -(1 << 20);
+    d_h[j] = ho * p.sh - p.ph;
+    d_w[j] = wo * p.sw - p.pw;
+    d_pix[j] = ((mt * p.Ti + d_t[j]) * p.Hi + d_h[j]) * p.Wi + d_w[j];
+  }
+  const __bf16* d_wrow[B_PER];
+#pragma unroll
+  for (int j = 0; j < B_PER; ++j) {
+    const int idx = wid + 4 * j;  // B instruction: piece idx / NT, rows 16 (idx % NT) ..
+    const int pc = idx / NT, nr = idx - pc * NT;
+    d_wrow[j] = idx < B_INS ? w + ((size_t)(n0 + nr * 16 + drow) * npairs * 3 + pc) * 32 + 8 * dq : w;
+  }
+  const int khw = p.KH * p.KW;
+  const int kmain = p.KT * khw * p.Cin;
+
+  const int kb = split * npairs / n_split, ke = (split + 1) * npairs / n_split;
+  int c_c0 = 0, c_kt = 0, c_kh = 0, c_kw = 0, c_tap_pix = 0;
+  bool c_second = kmain == 0;
+  if (kb > 0) {
+    const int e0 = kb * 32;
+    if (e0 >= kmain) {
+      c_second = true;
+      c_c0 = e0 - kmain;
+    } else {
+      const int tap = e0 / p.Cin;
+      c_c0 = e0 - tap * p.Cin;
+      c_kw = tap % p.KW;
+      c_kh = (tap / p.KW) % p.KH;
+      c_kt = tap / khw;
+      c_tap_pix = (c_kt * p.Hi + c_kh) * p.Wi + c_kw;
+    }
+  }
+  auto issue = [&](int pair, int slot) {
+    char* stg = smem + slot * STAGE;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const bool valid = 2 * pair + sub < nsteps;  // wave-uniform
+      const bool second = c_second;
+      const int cin = second ? p.Cin2 : p.Cin;
+      const float* xb = second ? x2 : x;
+      const int c0 = c_c0, kt = c_kt, kh = c_kh, kw = c_kw, tap_pix = c_tap_pix;
+      if (valid) {
+        c_c0 += 16;
+        if (c_c0 == cin) {
+          c_c0 = 0;
+          if (++c_kw == p.KW) {
+            c_kw = 0;
+            if (++c_kh == p.KH) {
+              c_kh = 0;
+              if (++c_kt == p.KT) c_kt = 0, c_second = true;
+            }
+          }
+          c_tap_pix = (c_kt * p.Hi + c_kh) * p.Wi + c_kw;
+        }
+      }
+      const float* xc = xb + c0 + 4 * dq;
+#pragma unroll
+      for (int j = 0; j < A_PER; ++j) {
+        const int ti = d_t[j] + kt, hi = d_h[j] + kh, wi = d_w[j] + kw;
+        const bool ok = valid & ((unsigned)ti < (unsigned)p.Ti) & ((unsigned)hi < (unsigned)p.Hi) &
+                        ((unsigned)wi < (unsigned)p.Wi);
+        const unsigned e = (unsigned)(d_pix[j] + tap_pix) * (unsigned)cin;
+        const void* src = ok ? (const void*)(xc + (size_t)e) : p.zero;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(stg + sub * A_BYTES +
+                                                                                   (wid * A_PER + j) * 1024),
+                                         16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < B_PER; ++j) {
+      const int idx = wid + 4 * j;
+      const void* src = idx < B_INS ? (const void*)(d_wrow[j] + (size_t)pair * 96) : p.zero;
+      char* dst = idx < B_INS ? stg + 2 * A_BYTES + idx * 1024 : smem + JUNK;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = ke - kb;
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(kb + s, s);
+
+  const int pq = q ^ G[l16 >> 2];
+  const int a_off = (wid * 16 * MT + l16) * 64 + pq * 16;
+  const int b_off = 2 * A_BYTES + l16 * 64 + pq * 16;
+  for (int k = 0; k < nk; ++k) {
+    if (k + S - 2 < nk) {
+      if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 * PER_WAVE) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (k + S - 1 < nk) issue(kb + k + S - 1, (k + S - 1) % S);
+    const char* st = smem + (k % S) * STAGE;
+    bf16x8 ah[MT], am[MT], al[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(st + a_off + i * 16 * 64);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(st + A_BYTES + a_off + i * 16 * 64);
+      split3_bf16x8(a0, a1, ah[i], am[i], al[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(st + b_off + j * 1024);
+      const bf16x8 bm = *reinterpret_cast<const bf16x8*>(st + b_off + (NT + j) * 1024);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(st + b_off + (2 * NT + j) * 1024);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        f32x4 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah[i], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al[i], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am[i], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah[i], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, am[i], c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah[i], c, 0, 0, 0);
+      }
+    }
+  }
+  if (n_split > 1)
+    partial_store<MT, NT>(p, acc, p.part + (size_t)split * p.M * p.Cout, m0 + wid * 16 * MT, n0, q, l16);
+  else
+    epilogue<MT, NT>(p, acc, m0 + wid * 16 * MT, n0, q, l16);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Register-staged variant for the stem's 1x7x7 conv over 3 (padded 4) fp32 input channels: the
 // 16-deep K slice spans 4 taps, decoded per float4. BM = 128, BN = 16*NT.
 template <int NT>
@@ -515,6 +726,17 @@ hipError_t launch_dma(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int MT, int NT, int S>
+hipError_t launch_dma_x3_t(const ConvParams& p, hipStream_t s) {
+  constexpr int BM = 64 * MT, BN = 16 * NT;
+  const int mt = (p.M + BM - 1) / BM, nt = (p.Cout + BN - 1) / BN;
+  const DmaDivs dv{fast_div(p.Wo), fast_div(p.Ho), fast_div(p.To), fast_div(nt)};
+  const int n_split = p.n_split > 1 ? p.n_split : 1;
+  hipLaunchKernelGGL((conv_dma_x3<MT, NT, S>), dim3(mt * nt * n_split), dim3(256), 0, s, p, nt, dv);
+  if (n_split > 1) return launch_split_sum(p, s);
+  return hipGetLastError();
+}
+
 template <int NT>
 hipError_t launch_stem(const ConvParams& p, hipStream_t s) {
   if (p.Cin != 4 || p.KT != 1 || p.KH != 7 || p.KW != 7) return hipErrorInvalidValue;  // conv_stem_f32's geometry
@@ -551,6 +773,63 @@ hipError_t launch_bf16_m4(const ConvParams& p, int bn, hipStream_t s) {
 }
 
 }  // namespace
+
+// conv_dma_x3 (fp32 engines, non-stem implicit-GEMM convs): fp32 activations in, fp32 out
+bool dma_x3_supported(const ConvParams& p) {
+  return !(p.vflags & CLASFV_VARIANT_NO_DMA_X3) && !p.in_bf16 && !p.out_bf16 && !p.stem && !p.x_c8 && !p.y_c8 &&
+         p.Kp % 16 == 0 && p.Cin % 16 == 0 && (!p.x2 || p.Cin2 % 16 == 0) && p.Cout % 16 == 0;
+}
+
+// N tile of conv_dma_x3: the widest 16*NT (NT <= 6: a stage is (16 MT + 3 NT) KiB, two per block,
+// two blocks per CU) dividing Cout
+int dma_x3_bn(int cout_p) {
+  const int n16 = cout_p / 16;
+  for (int c : {6, 5, 4, 3})
+    if (n16 % c == 0) return 16 * c;
+  return 16 * (n16 % 2 == 0 ? 2 : 1);
+}
+
+hipError_t launch_dma_x3(const ConvParams& p, int bn, hipStream_t s) {
+  if (!dma_x3_supported(p)) return hipErrorInvalidValue;
+  switch (bn) {
+    case 16: return launch_dma_x3_t<2, 1, 2>(p, s);
+    case 32: return launch_dma_x3_t<2, 2, 2>(p, s);
+    case 48: return launch_dma_x3_t<2, 3, 2>(p, s);
+    case 64: return launch_dma_x3_t<2, 4, 2>(p, s);
+    case 80: return launch_dma_x3_t<2, 5, 2>(p, s);
+    case 96: return launch_dma_x3_t<2, 6, 2>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+// bf16 image [cout_alloc][npairs][3][32] of an fp32 [cout_alloc][Kp] weight image (Kp % 16 == 0,
+// npairs = ceil(Kp / 32)): piece pc of element (n, k) is the bf16 of w - (pieces < pc) (round to
+// nearest, exact in double); element 8q + e of a 32-slot holds k = 32 pair + 4q + e (e < 4) or
+// 32 pair + 16 + 4q + (e - 4) -- conv_dma_x3's operand order.
+void dma_x3_weight_image(const float* w, int cout_alloc, int Kp, uint16_t* out) {
+  const int npairs = (Kp / 16 + 1) / 2;
+  for (int n = 0; n < cout_alloc; ++n)
+    for (int pr = 0; pr < npairs; ++pr)
+      for (int sl = 0; sl < 32; ++sl) {
+        const int q = sl >> 3, e = sl & 7;
+        const int k = 32 * pr + (e < 4 ? 4 * q + e : 16 + 4 * q + (e - 4));
+        double r = k < Kp ? (double)w[(size_t)n * Kp + k] : 0.0;
+        for (int pc = 0; pc < 3; ++pc) {
+          float f = (float)r;
+          uint32_t u;
+          memcpy(&u, &f, 4);
+          // round to nearest even on the upper 16 bits (finite weights)
+          const uint16_t b = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+          const uint32_t ub = (uint32_t)b << 16;
+          float fb;
+          memcpy(&fb, &ub, 4);
+          out[(((size_t)n * npairs + pr) * 3 + pc) * 32 + sl] = b;
+          r -= fb;
+        }
+      }
+}
+
+size_t dma_x3_weight_elems(int cout_alloc, int Kp) { return (size_t)cout_alloc * ((Kp / 16 + 1) / 2) * 96; }
 
 // Tile choice: BM = 128 (mt = 2) and the widest N tile (16*NT, NT <= 9) dividing Cout.
 // Measured (round 1, 30 clips of 32x112x112): BM = 128 beats 64 and 256 on every layer -- 256 halves

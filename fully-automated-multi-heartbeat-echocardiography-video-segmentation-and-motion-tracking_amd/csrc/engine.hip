@@ -81,6 +81,7 @@ struct Conv {
   float* dwino4 = nullptr;  // Winograd F(4x4,3x3) transformed weights (the same convs, cout_p % 48 == 0)
   float* dwinot = nullptr;  // Winograd F(4,3)-in-time transformed weights (fp32 stride-1 3x1x1 convs)
   void* dws16 = nullptr;    // bf16 stem weights, hi and lo images [64][7 kh][8 kw][4 c] (bf16 engines)
+  void* dx3 = nullptr;      // fp32 engines' implicit-GEMM convs: 3-piece bf16 image for conv_dma_x3
 };
 
 // fp32 stride-1 3x1x1 convs run on the fused temporal Winograd kernel, fp32 stride-1 1x3x3 convs on
@@ -114,6 +115,7 @@ int env_variants() {
   if (on("CLASFV_NO_SPLIT_K")) f |= CLASFV_VARIANT_NO_SPLIT_K;
   if (on("CLASFV_NO_WINO4")) f |= CLASFV_VARIANT_NO_WINO4;
   if (on("CLASFV_NO_DECODER_X3")) f |= CLASFV_VARIANT_NO_DECODER_X3;
+  if (on("CLASFV_NO_DMA_X3")) f |= CLASFV_VARIANT_NO_DMA_X3;
   return f;
 }
 
@@ -304,6 +306,12 @@ int upload_conv(Conv& c, F wsrc, const std::vector<double>& scale, const std::ve
         w[(size_t)o * c.Kp + (size_t)tap * c.cin_p + ci] = (float)((double)wsrc(o, ci, tap) * scale[o]);
   int rc = c.in_bf16 ? upload_bf16(w, &c.dw) : upload(w, reinterpret_cast<float**>(&c.dw));
   if (rc) return rc;
+  if (!c.in_bf16 && !c.stem && c.Kp % 16 == 0) {  // conv_dma_x3's split image of the same weights
+    std::vector<uint16_t> x3(dma_x3_weight_elems(c.cout_alloc, c.Kp));
+    dma_x3_weight_image(w.data(), c.cout_alloc, c.Kp, x3.data());
+    HIP_TRY(hipMalloc(&c.dx3, x3.size() * sizeof(uint16_t)));
+    HIP_TRY(hipMemcpy(c.dx3, x3.data(), x3.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+  }
   if (has_bias) {
     std::vector<float> b(c.cout_alloc, 0.f);
     for (int o = 0; o < c.cout; ++o) b[o] = (float)shift[o];
@@ -349,6 +357,10 @@ double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
     return 2.0 * out.n * ((out.t + fr - 1) / fr * fr) * px * c.cout_p * (double)c.Kp * 1e-9;
   }
   const double m = (double)out.n * out.t * out.h * out.w;
+  // conv_dma_x3: the fp32 GEMM it computes (K padded to 32-deep pairs), priced like the fp32 MFMA
+  // kernels; its six bf16 products per K block run on the bf16 matrix rate
+  if (!strcmp(kname, "conv_dma_x3"))
+    return 2.0 * (ceil(m / 128.0) * 128.0) * c.cout_p * (double)((c.Kp + 31) / 32 * 32) * 1e-9;
   return 2.0 * (ceil(m / 128.0) * 128.0) * c.cout_p * (double)c.Kp * 1e-9;
 }
 
@@ -385,6 +397,7 @@ const char* pick_kernel(const Conv& c, ConvParams p) {
   if (c.dws16 && !(p.vflags & CLASFV_VARIANT_NO_STEM_BF16) && stem_bf16_supported(p)) return "conv_stem_bf16";
   if (c.dwinot && winot_supported(p)) return "conv_winot";
   if (!(p.vflags & CLASFV_VARIANT_NO_PATCH_BF16) && patch_bf16_supported(p)) return "conv_patch_bf16";
+  if (c.dx3 && dma_x3_supported(p)) return "conv_dma_x3";
   return c.stem ? "conv_stem_f32" : "conv_dma";
 }
 
@@ -450,6 +463,14 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
     HIP_TRY(launch_winot(p, s));
   } else if (!strcmp(k, "conv_patch_bf16")) {
     HIP_TRY(launch_patch_bf16(p, s));
+  } else if (!strcmp(k, "conv_dma_x3")) {
+    p.w = c.dx3;
+    const int S = dma_split_for(p, 2);
+    if (S > 1 && scratch && (size_t)S * p.M * p.Cout * sizeof(float) <= scratch_bytes) {
+      p.part = reinterpret_cast<float*>(scratch);
+      p.n_split = S;
+    }
+    HIP_TRY(launch_dma_x3(p, dma_x3_bn(c.cout_p), s));
   } else {
     int mt = 2, bn = c.cout_p;  // stem: one N tile (48 fp32 / 64 bf16 channels)
     if (!c.stem) {
@@ -572,8 +593,12 @@ int clasfv_destroy(clasfv_t h) {
     (void)hipFree(c.dwino4);
     (void)hipFree(c.dwinot);
     (void)hipFree(c.dws16);
+    (void)hipFree(c.dx3);
   }
-  for (auto& c : h->proj) (void)hipFree(c.dw);
+  for (auto& c : h->proj) {
+    (void)hipFree(c.dw);
+    (void)hipFree(c.dx3);
+  }
   if (h->side) (void)hipStreamDestroy(h->side);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
@@ -638,7 +663,8 @@ int clasfv_finalize(clasfv_t h) {
     (void)hipFree(c.dwino4);
     (void)hipFree(c.dwinot);
     (void)hipFree(c.dws16);
-    c.dw = c.dws16 = nullptr;
+    (void)hipFree(c.dx3);
+    c.dw = c.dws16 = c.dx3 = nullptr;
     c.db = nullptr;
     c.dwino = c.dwino4 = c.dwinot = nullptr;
     bn_scale_shift(h, c.bn, c.cout, s, t);
@@ -697,7 +723,8 @@ int clasfv_finalize(clasfv_t h) {
     if (i == 1) continue;  // folded into the dual proj[0]
     Conv& c = h->proj[i];
     (void)hipFree(c.dw);
-    c.dw = nullptr;
+    (void)hipFree(c.dx3);
+    c.dw = c.dx3 = nullptr;
     const int o0 = col0[i];
     const int kin = c.cin + c.cin2;
     Conv tmp = c;  // upload_conv walks cin: give it the concatenated width
@@ -706,6 +733,7 @@ int clasfv_finalize(clasfv_t h) {
         tmp, [&](int o, int ci, int) { return w1[(size_t)o * 1024 + o0 + ci]; }, s, zero, false);
     if (rc) return rc;
     c.dw = tmp.dw;
+    c.dx3 = tmp.dx3;
   }
   std::vector<float> b1(64);
   for (int o = 0; o < 64; ++o) b1[o] = (float)(s[o] * (double)bias1[o] + t[o]);
@@ -788,7 +816,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0x7FF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~0xFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;
@@ -944,7 +972,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   // comb_2 (64x64; three split-bf16 products in bf16 engines, six in fp32 ones) and the heads (6
   // useful of the 16 rows of their MFMA tile) per output voxel
   timed("decoder_kernel", 2.0 * N * (double)T * H * W * (64 * 64 + 64 * 6) * 1e-9,
-        2.0 * N * (double)T * H * W * ((d.bf16 ? 3 : d.x3 ? 6 : 1) * 64 * 64 + 64 * 16) * 1e-9);
+        2.0 * N * (double)T * H * W * ((d.bf16 ? 3 : 1) * 64 * 64 + 64 * 16) * 1e-9);
   return CLASFV_OK;
 }
 

@@ -597,6 +597,26 @@ def test_decoder_x3_matches_fp32_mfma(model, shape):
     np.testing.assert_allclose(m3.cpu().numpy(), m1.cpu().numpy(), rtol=0, atol=MOT_ATOL / 4)
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (3, 3, 8, 32, 48)])
+def test_dma_x3_matches_fp32_mfma(model, shape):
+    """The fp32 engines' strided / 1x1x1 convs and decoder projections on conv_dma_x3 (six
+    split-bf16 products per K block, fp32 accumulation) against conv_dma on fp32 MFMAs (variant
+    no_dma_x3): the same GEMMs to fp32 rounding, so the forward stays within the fp32 bar and the
+    mask labels agree except at that rounding level."""
+    rng = np.random.default_rng(47)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    s3, m3 = model(x)
+    model.set_kernel_variants("no_dma_x3")
+    s1, m1 = model(x)
+    model.set_kernel_variants()
+    assert not torch.equal(s3, s1)  # the split-bf16 GEMM really ran
+    np.testing.assert_allclose(s3.cpu().numpy(), s1.cpu().numpy(), rtol=0, atol=SEG_ATOL)
+    np.testing.assert_allclose(m3.cpu().numpy(), m1.cpu().numpy(), rtol=0, atol=MOT_ATOL)
+    d = (s3[:, 1] - s3[:, 0]).cpu().numpy()
+    flips = ((s3[:, 1] > s3[:, 0]) != (s1[:, 1] > s1[:, 0])).cpu().numpy()
+    assert np.all(np.abs(d[flips]) <= 2 * SEG_ATOL)
+
+
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (1, 3, 8, 32, 48)])
 def test_c8_blocked_mid_bitexact(model, shape):
     """The 8-channel-blocked mid tensors (stem and Conv2Plus1D spatial -> temporal Winograd) only

@@ -117,8 +117,20 @@ int main(int argc, char** argv) {
   p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
   p.res = (getenv("CB_NORES") || wino4) ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
   CK(hipMalloc(&p.y, ny * 4));
+  // ko 710..719 (fp32 direct convs): conv_dma_x3 on the split-bf16 image of the same weights,
+  // split-K into ko - 710 K ranges when >= 2
+  void* wx3 = nullptr;
   for (int ko : kos)
-    if (((winot && ko >= 600 && ko < 700) || (!wino && !winot && ko >= 700 && ko < 709)) && !p.part)
+    if (!wino && !winot && !bf && ko >= 710 && ko < 720 && !wx3) {
+      std::vector<float> wf(nw);
+      CK(hipMemcpy(wf.data(), p.w, nw * 4, hipMemcpyDeviceToHost));
+      std::vector<uint16_t> img(dma_x3_weight_elems(Cout, p.Kp));
+      dma_x3_weight_image(wf.data(), Cout, p.Kp, img.data());
+      CK(hipMalloc(&wx3, img.size() * 2));
+      CK(hipMemcpy(wx3, img.data(), img.size() * 2, hipMemcpyHostToDevice));
+    }
+  for (int ko : kos)
+    if (((winot && ko >= 600 && ko < 700) || (!wino && !winot && ko >= 700 && ko < 720)) && !p.part)
       CK(hipMalloc((void**)&p.part, 8 * ny * 4));  // split-K partials
   void* z;
   CK(hipMalloc(&z, 256));
@@ -145,7 +157,13 @@ int main(int argc, char** argv) {
       if (getenv("CB_MT")) mt = atoi(getenv("CB_MT"));
       ConvParams q = p;
       if (ko >= 700 && ko < 709) q.n_split = ko - 700;  // conv_dma split-K into ko - 700 K ranges
-      CK(launch_conv(q, mt, bn, s));
+      if (ko >= 710 && ko < 720) {
+        q.w = wx3;
+        q.n_split = ko - 710;
+        CK(launch_dma_x3(q, getenv("CB_NT") ? 16 * atoi(getenv("CB_NT")) : dma_x3_bn(Cout), s));
+      } else {
+        CK(launch_conv(q, mt, bn, s));
+      }
     }
   };
   // warm every variant up (clocks settle), then interleave 3 timed rounds and keep each one's best
