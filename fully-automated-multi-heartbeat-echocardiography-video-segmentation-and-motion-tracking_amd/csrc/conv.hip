@@ -333,8 +333,9 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
   static_assert(A_INS % 4 == 0, "A rows split evenly over the 4 waves");
   constexpr int A_BYTES = A_INS * 1024;
   constexpr int STAGE = (2 * A_INS + B_INS) * 1024;
-  constexpr int JUNK = S * STAGE;
-  __shared__ __align__(16) char smem[S * STAGE + 1024];
+  constexpr int JUNK = S * STAGE;  // 1 KB sink for the padding DMAs, when B_INS % 4 != 0
+  constexpr int SINK = B_INS % 4 ? 1024 : 0;  // (N tile 128: 2 x 80 KB blocks per CU)
+  __shared__ __align__(16) char smem[S * STAGE + SINK];
 
   const float* x = reinterpret_cast<const float*>(p.x);
   const float* x2 = reinterpret_cast<const float*>(p.x2);
@@ -780,11 +781,11 @@ bool dma_x3_supported(const ConvParams& p) {
          p.Kp % 16 == 0 && p.Cin % 16 == 0 && (!p.x2 || p.Cin2 % 16 == 0) && p.Cout % 16 == 0;
 }
 
-// N tile of conv_dma_x3: the widest 16*NT (NT <= 6: a stage is (16 MT + 3 NT) KiB, two per block,
-// two blocks per CU) dividing Cout
+// N tile of conv_dma_x3: the widest 16*NT (NT = 8 or <= 6: a stage is (16 MT + 3 NT) KiB, two per
+// block, two blocks per CU) dividing Cout
 int dma_x3_bn(int cout_p) {
   const int n16 = cout_p / 16;
-  for (int c : {6, 5, 4, 3})
+  for (int c : {8, 6, 5, 4, 3})
     if (n16 % c == 0) return 16 * c;
   return 16 * (n16 % 2 == 0 ? 2 : 1);
 }
@@ -798,9 +799,29 @@ hipError_t launch_dma_x3(const ConvParams& p, int bn, hipStream_t s) {
     case 64: return launch_dma_x3_t<2, 4, 2>(p, s);
     case 80: return launch_dma_x3_t<2, 5, 2>(p, s);
     case 96: return launch_dma_x3_t<2, 6, 2>(p, s);
+    case 128: return launch_dma_x3_t<2, 8, 2>(p, s);
   }
   return hipErrorInvalidValue;
 }
+
+#ifdef CLASFV_KNOCKOUTS
+// tools/convbench.hip: conv_dma_x3 tile / ring experiments (M tile 64*mt, N tile 16*nt, S stages)
+hipError_t launch_dma_x3_cfg(const ConvParams& p, int mt, int nt, int S, hipStream_t s) {
+  const int key = mt * 100 + nt * 10 + S;
+  switch (key) {
+    case 132: return launch_dma_x3_t<1, 3, 2>(p, s);
+    case 133: return launch_dma_x3_t<1, 3, 3>(p, s);
+    case 162: return launch_dma_x3_t<1, 6, 2>(p, s);
+    case 163: return launch_dma_x3_t<1, 6, 3>(p, s);
+    case 233: return launch_dma_x3_t<2, 3, 3>(p, s);
+    case 243: return launch_dma_x3_t<2, 4, 3>(p, s);
+    case 263: return launch_dma_x3_t<2, 6, 3>(p, s);
+    case 432: return launch_dma_x3_t<4, 3, 2>(p, s);
+    case 462: return launch_dma_x3_t<4, 6, 2>(p, s);
+  }
+  return launch_dma_x3(p, 16 * nt, s);
+}
+#endif
 
 // bf16 image [cout_alloc][npairs][3][32] of an fp32 [cout_alloc][Kp] weight image (Kp % 16 == 0,
 // npairs = ceil(Kp / 32)): piece pc of element (n, k) is the bf16 of w - (pieces < pc) (round to

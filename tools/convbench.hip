@@ -20,6 +20,7 @@ hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_wino4_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winor_ko(const ConvParams& p, hipStream_t s, int ko);
+hipError_t launch_dma_x3_cfg(const ConvParams& p, int mt, int nt, int S, hipStream_t s);
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
 hipError_t launch_patch_bf16_v1(const ConvParams& p, hipStream_t s);
 hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
@@ -160,7 +161,10 @@ int main(int argc, char** argv) {
       if (ko >= 710 && ko < 720) {
         q.w = wx3;
         q.n_split = ko - 710;
-        CK(launch_dma_x3(q, getenv("CB_NT") ? 16 * atoi(getenv("CB_NT")) : dma_x3_bn(Cout), s));
+        const char* cfg = getenv("CB_X3CFG");  // "MT NT S"
+        int xm = 2, xn = dma_x3_bn(Cout) / 16, xs = 2;
+        if (cfg && *cfg) sscanf(cfg, "%d %d %d", &xm, &xn, &xs);
+        CK(launch_dma_x3_cfg(q, xm, xn, xs, s));
       } else {
         CK(launch_conv(q, mt, bn, s));
       }
