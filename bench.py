@@ -178,7 +178,7 @@ def kernel_roofline(ktimes, peak, dtype):
             "traffic_source": tr and tr["source"],
             "note": "achieved = MFMA work issued (Winograd F(4x4,3x3): 36 of the 144 direct products per 4x4 "
                     "tile, 16-tile MFMA groups; F(2x2,3x3): 16 of 36 per 2x2 tile; F(4,3): 6 of 12 per 4 frames; "
-                    "padded channels and partial tiles counted) / time; algorithmic_equiv_tflops = the direct-"
+                    "padded channels and partial tiles counted; split-bf16 kernels: the fp32 GEMM they compute) / time; algorithmic_equiv_tflops = the direct-"
                     "convolution FLOPs of the same launches / time"}
 
 
@@ -479,6 +479,10 @@ def run_c1(args, model, world, rank, dev):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
+        "dtype_note": ("fp32 activations, weights and accumulation; Winograd / stem convs on f32 MFMAs, "
+                       "strided / 1x1x1 convs, projections and comb_2 on split-bf16 MFMAs (3 bf16 pieces "
+                       "per operand, 6 products, fp32 accumulation: fp32-accurate; variants no_dma_x3 / "
+                       "no_decoder_x3 run them on f32 MFMAs)") if args.dtype == "fp32" else None,
         "data": "synthetic EchoNet-style video (seeded), seeded synthetic weights (" + BENCH_WEIGHTS + " recipe)",
         "config": {"workload": "BASELINE config[1] per GPU: 200-frame 112x112 video, 5 shifted passes "
                                "(30 x 32-frame clips) + per-frame SIMPLE label fusion",
