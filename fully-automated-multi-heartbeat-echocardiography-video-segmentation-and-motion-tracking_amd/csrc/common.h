@@ -111,6 +111,9 @@ bool winot_c8_ok(const ConvParams& p);
 hipError_t launch_split_sum(const ConvParams& p, hipStream_t s);
 // Split-K factor for launch_conv's conv_dma with M tile mt (1: no split; per-clip shape only).
 int dma_split_for(const ConvParams& p, int mt);
+// conv_stem_x3: the fp32 engines' stem on split-bf16 MFMAs (conv.hip)
+bool stem_x3_supported(const ConvParams& p);
+hipError_t launch_stem_x3(const ConvParams& p, hipStream_t s);
 // conv_dma_x3: fp32 implicit GEMM on split-bf16 MFMAs (six products, fp32-accurate; conv.hip)
 bool dma_x3_supported(const ConvParams& p);
 int dma_x3_bn(int cout_p);

@@ -324,8 +324,12 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
 // (64-B rows, swizzled slots), B as 3 pieces x BN rows of 64 B (32 bf16: slot q holds, for lane group
 // q, k = 4q..4q+3 of the first step and of the second), so lane (l16, q) builds its 8-element bf16
 // operands from its f32x4 slot of each step -- the same k set on both sides of the product.
-template <int MT, int NT, int S>
+// WN: waves along N (1: 4 waves x (BM/4 rows x BN); 2: 2 x 2 waves of (BM/2 rows x BN/2), halving the
+// B-piece LDS reads per wave at twice the A splits).
+template <int MT, int NT, int S, int WN = 1>
 __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, DmaDivs dv) {
+  static_assert(NT % WN == 0, "N tiles split evenly over the waves along N");
+  constexpr int MTW = MT * WN, NTW = NT / WN;  // 16 x 16 tiles per wave
   constexpr int BM = 64 * MT, BN = 16 * NT;
   constexpr int A_INS = BM / 16, B_INS = 3 * NT;     // DMA instructions (16 rows x 64 B) per step / pair
   constexpr int A_PER = A_INS / 4, B_PER = (B_INS + 3) / 4;
@@ -444,20 +448,21 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
     }
   };
 
-  f32x4 acc[MT][NT];
+  f32x4 acc[MTW][NTW];
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+  for (int i = 0; i < MTW; ++i)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = ke - kb;
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(kb + s, s);
 
+  const int wm = wid % (4 / WN), wn = wid / (4 / WN);
   const int pq = q ^ G[l16 >> 2];
-  const int a_off = (wid * 16 * MT + l16) * 64 + pq * 16;
-  const int b_off = 2 * A_BYTES + l16 * 64 + pq * 16;
+  const int a_off = (wm * 16 * MTW + l16) * 64 + pq * 16;
+  const int b_off = 2 * A_BYTES + (wn * NTW) * 1024 + l16 * 64 + pq * 16;
   for (int k = 0; k < nk; ++k) {
     if (k + S - 2 < nk) {
       if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -470,20 +475,20 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
     __builtin_amdgcn_sched_barrier(0);
     if (k + S - 1 < nk) issue(kb + k + S - 1, (k + S - 1) % S);
     const char* st = smem + (k % S) * STAGE;
-    bf16x8 ah[MT], am[MT], al[MT];
+    bf16x8 ah[MTW], am[MTW], al[MTW];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
+    for (int i = 0; i < MTW; ++i) {
       const f32x4 a0 = *reinterpret_cast<const f32x4*>(st + a_off + i * 16 * 64);
       const f32x4 a1 = *reinterpret_cast<const f32x4*>(st + A_BYTES + a_off + i * 16 * 64);
       split3_bf16x8(a0, a1, ah[i], am[i], al[i]);
     }
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
+    for (int j = 0; j < NTW; ++j) {
       const bf16x8 bh = *reinterpret_cast<const bf16x8*>(st + b_off + j * 1024);
       const bf16x8 bm = *reinterpret_cast<const bf16x8*>(st + b_off + (NT + j) * 1024);
       const bf16x8 bl = *reinterpret_cast<const bf16x8*>(st + b_off + (2 * NT + j) * 1024);
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
+      for (int i = 0; i < MTW; ++i) {
         f32x4 c = acc[i][j];
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah[i], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al[i], c, 0, 0, 0);
@@ -495,9 +500,10 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
     }
   }
   if (n_split > 1)
-    partial_store<MT, NT>(p, acc, p.part + (size_t)split * p.M * p.Cout, m0 + wid * 16 * MT, n0, q, l16);
+    partial_store<MTW, NTW>(p, acc, p.part + (size_t)split * p.M * p.Cout, m0 + wm * 16 * MTW, n0 + wn * 16 * NTW, q,
+                            l16);
   else
-    epilogue<MT, NT>(p, acc, m0 + wid * 16 * MT, n0, q, l16);
+    epilogue<MTW, NTW>(p, acc, m0 + wm * 16 * MTW, n0 + wn * 16 * NTW, q, l16);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -727,13 +733,13 @@ hipError_t launch_dma(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int MT, int NT, int S>
+template <int MT, int NT, int S, int WN = 1>
 hipError_t launch_dma_x3_t(const ConvParams& p, hipStream_t s) {
   constexpr int BM = 64 * MT, BN = 16 * NT;
   const int mt = (p.M + BM - 1) / BM, nt = (p.Cout + BN - 1) / BN;
   const DmaDivs dv{fast_div(p.Wo), fast_div(p.Ho), fast_div(p.To), fast_div(nt)};
   const int n_split = p.n_split > 1 ? p.n_split : 1;
-  hipLaunchKernelGGL((conv_dma_x3<MT, NT, S>), dim3(mt * nt * n_split), dim3(256), 0, s, p, nt, dv);
+  hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN>), dim3(mt * nt * n_split), dim3(256), 0, s, p, nt, dv);
   if (n_split > 1) return launch_split_sum(p, s);
   return hipGetLastError();
 }
@@ -773,6 +779,81 @@ hipError_t launch_bf16_m4(const ConvParams& p, int bn, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
+// fp32-engine stem on split-bf16 MFMAs (conv_stem_x3): conv_stem_bf16's structure and K order with
+// three bf16 pieces per operand (x = hi + mid + lo, fp32's 24 bits) and the six products of
+// conv_dma_x3, fp32 accumulation, 48 output channels (45 + 3 zero), fp32 output through the shared
+// epilogue (channels-last or 8-channel-blocked for the temporal Winograd after it). Weights: hi, mid
+// and lo images [48][7 kh][8 kw][4 c] bf16 (engine.hip, clasfv_finalize).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_stem_x3(ConvParams p) {
+  constexpr int MT = 4, NT = 3, CO = 16 * NT, ROW = 7 * 64, IMG = CO * ROW;
+  __shared__ __align__(16) char ws[3 * IMG];  // hi, mid, lo images
+  const float* x = reinterpret_cast<const float*>(p.x);
+  const char* w16 = reinterpret_cast<const char*>(p.w);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int q = lane >> 4, l16 = lane & 15;
+  const int m0 = xcd_swizzle(blockIdx.x, gridDim.x) * 256 + wid * 64;
+  for (int e = tid; e < 3 * CO * 28; e += 256) {  // [img][co][kh][slot] 16-B pieces, slot ^ (co & 3)
+    const int im = e / (CO * 28), r0 = e - im * (CO * 28);
+    const int co = r0 / 28, r = r0 - co * 28, kh = r >> 2, sl = r & 3;
+    *reinterpret_cast<uint4*>(ws + im * IMG + co * ROW + kh * 64 + ((sl ^ (co & 3)) << 4)) =
+        *reinterpret_cast<const uint4*>(w16 + (size_t)im * CO * 448 + (size_t)co * 448 + kh * 64 + sl * 16);
+  }
+  __syncthreads();
+  const int b_rd = l16 * ROW + ((q ^ (l16 & 3)) << 4);
+  const float* rowp[MT];
+  int hi0[MT], wi0[MT];
+  bool live[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    int m = m0 + 16 * i + l16;
+    live[i] = m < p.M;
+    if (!live[i]) m = 0;
+    const int wo = m % p.Wo;
+    m /= p.Wo;
+    const int ho = m % p.Ho;
+    const int nt = m / p.Ho;  // n * To + t (stride 1 in time, no temporal padding)
+    hi0[i] = 2 * ho - 3;
+    wi0[i] = 2 * wo - 3 + 2 * q;
+    rowp[i] = x + ((size_t)nt * p.Hi * p.Wi) * 4;
+  }
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int kh = 0; kh < 7; ++kh) {
+    bf16x8 ah[MT], am[MT], al[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int hi = hi0[i] + kh;
+      const bool rok = live[i] && (unsigned)hi < (unsigned)p.Hi;
+      const float* px = rowp[i] + ((size_t)hi * p.Wi + wi0[i]) * 4;
+      f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+      if (rok && (unsigned)wi0[i] < (unsigned)p.Wi) v0 = *reinterpret_cast<const f32x4*>(px);
+      if (rok && (unsigned)(wi0[i] + 1) < (unsigned)p.Wi) v1 = *reinterpret_cast<const f32x4*>(px + 4);
+      split3_bf16x8(v0, v1, ah[i], am[i], al[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(ws + j * 16 * ROW + kh * 64 + b_rd);
+      const bf16x8 bm = *reinterpret_cast<const bf16x8*>(ws + IMG + j * 16 * ROW + kh * 64 + b_rd);
+      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(ws + 2 * IMG + j * 16 * ROW + kh * 64 + b_rd);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        f32x4 c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah[i], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al[i], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am[i], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah[i], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, am[i], c, 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah[i], c, 0, 0, 0);
+      }
+    }
+  }
+  epilogue<MT, NT>(p, acc, m0, 0, q, l16);
+}
+
 }  // namespace
 
 // conv_dma_x3 (fp32 engines, non-stem implicit-GEMM convs): fp32 activations in, fp32 out
@@ -807,8 +888,13 @@ hipError_t launch_dma_x3(const ConvParams& p, int bn, hipStream_t s) {
 #ifdef CLASFV_KNOCKOUTS
 // tools/convbench.hip: conv_dma_x3 tile / ring experiments (M tile 64*mt, N tile 16*nt, S stages)
 hipError_t launch_dma_x3_cfg(const ConvParams& p, int mt, int nt, int S, hipStream_t s) {
-  const int key = mt * 100 + nt * 10 + S;
+  const int wn = getenv("CB_X3WN") ? atoi(getenv("CB_X3WN")) : 1;
+  const int key = (wn == 2 ? 1000 : 0) + mt * 100 + nt * 10 + S;
   switch (key) {
+    case 1242: return launch_dma_x3_t<2, 4, 2, 2>(p, s);
+    case 1262: return launch_dma_x3_t<2, 6, 2, 2>(p, s);
+    case 1282: return launch_dma_x3_t<2, 8, 2, 2>(p, s);
+    case 1162: return launch_dma_x3_t<1, 6, 2, 2>(p, s);
     case 132: return launch_dma_x3_t<1, 3, 2>(p, s);
     case 133: return launch_dma_x3_t<1, 3, 3>(p, s);
     case 162: return launch_dma_x3_t<1, 6, 2>(p, s);
@@ -941,6 +1027,19 @@ bool stem_bf16_supported(const ConvParams& p) {
   return p.stem && p.out_bf16 && p.Cin == 4 && p.Cout == 64 && p.KT == 1 && p.KH == 7 && p.KW == 7 && p.st == 1 &&
          p.sh == 2 && p.sw == 2 && p.pt == 0 && p.ph == 3 && p.pw == 3 && p.relu && !p.res && p.bias &&
          p.To == p.Ti && (size_t)p.M < ((size_t)1 << 31);
+}
+
+bool stem_x3_supported(const ConvParams& p) {
+  return !(p.vflags & CLASFV_VARIANT_NO_STEM_X3) && p.stem && !p.out_bf16 && !p.in_bf16 && p.Cin == 4 &&
+         p.Cout == 48 && p.KT == 1 && p.KH == 7 && p.KW == 7 && p.st == 1 && p.sh == 2 && p.sw == 2 && p.pt == 0 &&
+         p.ph == 3 && p.pw == 3 && !p.res && !p.x_c8 && p.To == p.Ti && (size_t)p.M < ((size_t)1 << 31);
+}
+
+// p.w: hi, mid, lo images, each [48][7 kh][8 kw][4 c] bf16 (engine.hip, clasfv_finalize).
+hipError_t launch_stem_x3(const ConvParams& p, hipStream_t s) {
+  if (!stem_x3_supported(p)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(conv_stem_x3, dim3((p.M + 255) / 256), dim3(256), 0, s, p);
+  return hipGetLastError();
 }
 
 // p.w: hi then lo image, each [64][7 kh][8 kw][4 c] bf16 (engine.hip, clasfv_finalize).

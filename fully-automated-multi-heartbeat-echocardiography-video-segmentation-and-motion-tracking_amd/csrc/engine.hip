@@ -80,7 +80,8 @@ struct Conv {
   float* dwino = nullptr;  // Winograd F(2x2,3x3) transformed weights (fp32 stride-1 1x3x3 convs)
   float* dwino4 = nullptr;  // Winograd F(4x4,3x3) transformed weights (the same convs, cout_p % 48 == 0)
   float* dwinot = nullptr;  // Winograd F(4,3)-in-time transformed weights (fp32 stride-1 3x1x1 convs)
-  void* dws16 = nullptr;    // bf16 stem weights, hi and lo images [64][7 kh][8 kw][4 c] (bf16 engines)
+  void* dws16 = nullptr;    // bf16 stem weights, hi and lo images [64][7 kh][8 kw][4 c] (bf16 engines);
+                            // fp32 engines: hi, mid and lo images [48][7][8][4] (conv_stem_x3)
   void* dx3 = nullptr;      // fp32 engines' implicit-GEMM convs: 3-piece bf16 image for conv_dma_x3
 };
 
@@ -116,6 +117,7 @@ int env_variants() {
   if (on("CLASFV_NO_WINO4")) f |= CLASFV_VARIANT_NO_WINO4;
   if (on("CLASFV_NO_DECODER_X3")) f |= CLASFV_VARIANT_NO_DECODER_X3;
   if (on("CLASFV_NO_DMA_X3")) f |= CLASFV_VARIANT_NO_DMA_X3;
+  if (on("CLASFV_NO_STEM_X3")) f |= CLASFV_VARIANT_NO_STEM_X3;
   return f;
 }
 
@@ -348,6 +350,8 @@ double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
   if (!strcmp(kname, "conv_wino_q") || !strcmp(kname, "conv_wino"))
     return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 1) / 2) * 16.0 * cc * 1e-9;
   if (!strcmp(kname, "conv_winot")) return 2.0 * out.n * (out.t / 4) * (double)out.h * out.w * 6.0 * cc * 1e-9;
+  if (!strcmp(kname, "conv_stem_x3"))  // the fp32 GEMM it computes (K = 7 rows x 8 taps x 4 channels)
+    return 2.0 * ceil((double)out.n * out.t * out.h * out.w / 256.0) * 256.0 * 48.0 * 224.0 * 1e-9;
   if (!strcmp(kname, "conv_stem_bf16"))
     return 3 * 2.0 * ceil((double)out.n * out.t * out.h * out.w / 256.0) * 256.0 * 64.0 * 224.0 * 1e-9;
   if (!strcmp(kname, "conv_patch_bf16")) {  // frames x 64-pixel tiles: 2 x 8x8 for 1x3x3, 4 x 64 flat for 3x1x1
@@ -395,6 +399,7 @@ const char* pick_kernel(const Conv& c, ConvParams p) {
     if (wino_supported(p)) return "conv_wino";
   }
   if (c.dws16 && !(p.vflags & CLASFV_VARIANT_NO_STEM_BF16) && stem_bf16_supported(p)) return "conv_stem_bf16";
+  if (c.dws16 && stem_x3_supported(p)) return "conv_stem_x3";
   if (c.dwinot && winot_supported(p)) return "conv_winot";
   if (!(p.vflags & CLASFV_VARIANT_NO_PATCH_BF16) && patch_bf16_supported(p)) return "conv_patch_bf16";
   if (c.dx3 && dma_x3_supported(p)) return "conv_dma_x3";
@@ -416,7 +421,8 @@ bool c8_pair(const Conv& a, const Conv& b, const Shape5& in, const Tuning& tu) {
   // Measured per producer (30 clips, profiles/r02j_*): stem and conv_wino_q (layer1, layer2) write
   // the blocked layout at no cost while the temporal kernels after them gain 7-24 %; conv_wino
   // (layer3) broke even and stays channels-last.
-  const bool writes = !strcmp(ka, "conv_wino4") || !strcmp(ka, "conv_wino_q") || !strcmp(ka, "conv_stem_f32");
+  const bool writes = !strcmp(ka, "conv_wino4") || !strcmp(ka, "conv_wino_q") || !strcmp(ka, "conv_stem_f32") ||
+                      !strcmp(ka, "conv_stem_x3");
   return writes && !a.out_bf16 && !strcmp(pick_kernel(b, pb), "conv_winot") && winot_c8_ok(pb);
 }
 
@@ -437,7 +443,8 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   p.y_c8 = y_c8;
   const char* k = pick_kernel(c, p);
   *kname = k;
-  const bool c8_out = !strcmp(k, "conv_wino4") || !strcmp(k, "conv_wino_q") || !strcmp(k, "conv_stem_f32");
+  const bool c8_out = !strcmp(k, "conv_wino4") || !strcmp(k, "conv_wino_q") || !strcmp(k, "conv_stem_f32") ||
+                      !strcmp(k, "conv_stem_x3");
   if ((y_c8 && !c8_out) || (x_c8 && strcmp(k, "conv_winot")))
     return fail(CLASFV_EINVAL, "internal: 8-channel-blocked layout on an unsupported kernel");
   if (!strcmp(k, "conv_wino4")) {
@@ -452,6 +459,9 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   } else if (!strcmp(k, "conv_stem_bf16")) {
     p.w = c.dws16;
     HIP_TRY(launch_stem_bf16(p, s));
+  } else if (!strcmp(k, "conv_stem_x3")) {
+    p.w = c.dws16;
+    HIP_TRY(launch_stem_x3(p, s));
   } else if (!strcmp(k, "conv_winot")) {
     p.w = c.dwinot;
     // split-K on the smallest maps (per-clip shape rule), partial sums in the caller's scratch
@@ -687,6 +697,25 @@ int clasfv_finalize(clasfv_t h) {
         if ((rc = upload(u4, &c.dwino4))) return rc;
       }
     }
+    if (!bf16 && c.stem && c.cout_p == 48 && c.kh == 7 && c.kw == 7 && cin <= 4) {  // conv_stem_x3's pieces
+      const size_t img = (size_t)48 * 7 * 8 * 4;
+      std::vector<float> ws(3 * img, 0.f);  // hi, mid, lo: bf16 of the remainder, in double
+      for (int o = 0; o < c.cout; ++o)
+        for (int ci = 0; ci < cin; ++ci)
+          for (int kh = 0; kh < 7; ++kh)
+            for (int kw = 0; kw < 7; ++kw) {
+              double r = (double)(float)((double)w[((size_t)o * cin + ci) * 49 + kh * 7 + kw] * s[o]);
+              const size_t k = (((size_t)o * 7 + kh) * 8 + kw) * 4 + ci;
+              for (int pc = 0; pc < 3; ++pc) {
+                const uint32_t hb = (uint32_t)to_bf16((float)r) << 16;
+                float f;
+                memcpy(&f, &hb, 4);
+                ws[pc * img + k] = f;
+                r -= f;
+              }
+            }
+      if ((rc = upload_bf16(ws, &c.dws16))) return rc;
+    }
     if (bf16 && c.stem && c.cout_p == 64 && c.kh == 7 && c.kw == 7 && cin <= 4) {  // conv_stem_bf16's K order
       const size_t img = (size_t)64 * 7 * 8 * 4;
       std::vector<float> ws(2 * img, 0.f);  // hi image, then lo = bf16(w - hi)
@@ -816,7 +845,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0xFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~0x1FFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;

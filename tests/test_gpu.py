@@ -597,16 +597,18 @@ def test_decoder_x3_matches_fp32_mfma(model, shape):
     np.testing.assert_allclose(m3.cpu().numpy(), m1.cpu().numpy(), rtol=0, atol=MOT_ATOL / 4)
 
 
+@pytest.mark.parametrize("variant", ["no_dma_x3", "no_stem_x3"])
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (3, 3, 8, 32, 48)])
-def test_dma_x3_matches_fp32_mfma(model, shape):
-    """The fp32 engines' strided / 1x1x1 convs and decoder projections on conv_dma_x3 (six
-    split-bf16 products per K block, fp32 accumulation) against conv_dma on fp32 MFMAs (variant
-    no_dma_x3): the same GEMMs to fp32 rounding, so the forward stays within the fp32 bar and the
-    mask labels agree except at that rounding level."""
+def test_x3_convs_match_fp32_mfma(model, shape, variant):
+    """The fp32 engines' split-bf16 convs (six bf16 products of 3-piece operands per K block, fp32
+    accumulation) against the same convs on fp32 MFMAs: conv_dma_x3 (strided / 1x1x1 convs, decoder
+    projections) vs conv_dma (variant no_dma_x3), conv_stem_x3 vs conv_stem_f32 (no_stem_x3). The
+    same GEMMs to fp32 rounding, so the forward stays within the fp32 bar and the mask labels agree
+    except at that rounding level."""
     rng = np.random.default_rng(47)
     x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
     s3, m3 = model(x)
-    model.set_kernel_variants("no_dma_x3")
+    model.set_kernel_variants(variant)
     s1, m1 = model(x)
     model.set_kernel_variants()
     assert not torch.equal(s3, s1)  # the split-bf16 GEMM really ran
