@@ -68,8 +68,8 @@ struct DecParams {
   DecTap tap[4];      // (stem+layer1), layer2, layer3, layer4
   const float* b1;    // [64]    comb_1 bias with BN1 folded
   const float* w2;    // [64*64] comb_2 weight with BN2 folded, [n][k]
-  const void* w2x3;   // fp32 engines: W2 as three bf16 pieces (hi, mid, lo: w2 = hi + mid + lo to 24
-                      // bits) in the MFMA lane order [3][nt 4][kb 2][l16 16][q 4][8], see decoder.hip
+  const void* w2x3;   // fp32 engines: W2 and Wh as three bf16 pieces (hi, mid, lo: w = hi + mid + lo to
+                      // 24 bits) in the MFMA lane order, decoder_x3_weights (decoder.hip)
   const float* b2;    // [64]
   const float* wh;    // [8*64]  rows: seg0, seg1, mot0..mot3, 0, 0
   const float* bh;    // [8]
@@ -134,4 +134,6 @@ hipError_t launch_patch_bf16(const ConvParams& p, hipStream_t s);
 bool stem_bf16_supported(const ConvParams& p);
 hipError_t launch_stem_bf16(const ConvParams& p, hipStream_t s);
 hipError_t launch_decoder(const DecParams& p, hipStream_t s);
+constexpr int DECODER_X3_ELEMS = 3 * 4096 + 3 * 1024;  // bf16 values of DecParams::w2x3
+void decoder_x3_weights(const float* w2, const float* wh, uint16_t* out);
 hipError_t launch_pack_input(const float* x, float* y, int N, int T, int HW, hipStream_t s);

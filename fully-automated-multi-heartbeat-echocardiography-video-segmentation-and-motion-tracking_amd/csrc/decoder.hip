@@ -23,6 +23,8 @@
 // loads, the blended staging and the occupancy).
 #include "common.h"
 
+#include <string.h>
+
 namespace {
 
 // floats per staged pixel: 64 channels + 8 pad. A ds_read_b128 lane group reads 8 distinct (source
@@ -122,7 +124,7 @@ __device__ inline void split3_bf16x8(f32x4 a, f32x4 b, bf16x8& hi, bf16x8& mid, 
 // accumulation -- fp32-accurate, on the bf16 matrix rate (12 instead of 32 MFMA slots; on gfx950 the
 // f32 MFMA shares the f32 vector rate with the interpolation, which the bf16 MFMA does not). W2's
 // pieces come split on the host (DecParams::w2x3), h1's are split here.
-template <bool X3>
+template <bool X3, bool HX3>
 __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[2][4], int t, int n, int h0, int w0,
                                           int wid, int q, int l16) {
   bf16x8 hh[2][2], hl[2][2], hm[2][2];
@@ -172,27 +174,51 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
       acc[mt][nt] = a;  // h2^T[ch = 16nt + 4q + r][voxel l16]
     }
   }
-  // heads in fp32 (they produce the logits whose sign is the mask): heads^T = Wh . h2^T on
-  // v_mfma_f32_16x16x4_f32, the accumulator layout being the B operand layout (k = 16nt + 4q + r)
-  f32x4 wh[4];
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    wh[nt] = *reinterpret_cast<const f32x4*>(p.wh + (l16 & 7) * 64 + 16 * nt + 4 * q);
-    if (l16 >= 8) wh[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
   f32x4 hb;
 #pragma unroll
   for (int r = 0; r < 4; ++r) hb[r] = 4 * q + r < 6 ? p.bh[4 * q + r] : 0.f;
   const size_t HW = (size_t)p.H * p.W;
   const size_t TH = (size_t)p.T * HW;
   f32x4 outs[2] = {hb, hb};  // head bias (rows 4q + r < 6) in the accumulator
+  if constexpr (HX3) {
+    // heads^T = Wh . h2^T as six split-bf16 products too: a lane's accumulators hold channels
+    // 16nt + 4q + r, i.e. K block kb = {nt 2kb, 2kb + 1} in the comb_2 operand order; Wh's pieces
+    // (16 rows, 6 used) come split on the host behind W2's (fp32-accurate; the f32 MFMAs they replace
+    // shared the f32 rate with the interpolation)
+    const bf16x8* h3 = reinterpret_cast<const bf16x8*>(p.w2x3) + 3 * 4096 / 8 + l16 * 4 + q;
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt)
+    for (int kb = 0; kb < 2; ++kb) {
+      const bf16x8 wh_ = h3[kb * 64], wm_ = h3[128 + kb * 64], wl_ = h3[256 + kb * 64];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+      for (int mt = 0; mt < 2; ++mt) {
+        bf16x8 vh, vm, vl;
+        split3_bf16x8(acc[mt][2 * kb], acc[mt][2 * kb + 1], vh, vm, vl);
+        f32x4 o = outs[mt];
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl_, vh, o, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh_, vl, o, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm_, vm, o, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm_, vh, o, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh_, vm, o, 0, 0, 0);
+        outs[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh_, vh, o, 0, 0, 0);
+      }
+    }
+  } else {
+    // heads in fp32 (they produce the logits whose sign is the mask): heads^T = Wh . h2^T on
+    // v_mfma_f32_16x16x4_f32, the accumulator layout being the B operand layout (k = 16nt + 4q + r)
+    f32x4 wh[4];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-        outs[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[mt][nt][r], outs[mt], 0, 0, 0);
+    for (int nt = 0; nt < 4; ++nt) {
+      wh[nt] = *reinterpret_cast<const f32x4*>(p.wh + (l16 & 7) * 64 + 16 * nt + 4 * q);
+      if (l16 >= 8) wh[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          outs[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wh[nt][r], acc[mt][nt][r], outs[mt], 0, 0, 0);
+  }
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt) {
     const int hr = h0 + 2 * wid + mt;
@@ -383,7 +409,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ?
       for (int j = 0; j < 4; ++j) h1[mt][c][j] = fmaxf(h1[mt][c][j], 0.f);
 
   if constexpr (BF) {
-    decoder_heads_bf16<MODE == 4>(p, h1, t, n, h0, w0, wid, q, l16);
+    decoder_heads_bf16<MODE == 4, true>(p, h1, t, n, h0, w0, wid, q, l16);
     return;
   }
   // 3. h2^T[n][v] = sum_k W2[n][k] h1[v][k]; MFMA j of lane group q covers k = 16c + 4q + j
@@ -488,8 +514,42 @@ static hipError_t launch_dec(const DecParams& p, hipStream_t s, int mode) {
   return hipGetLastError();
 }
 
+// DecParams::w2x3 of the X3 decoder: W2 (64 x 64, [n][k]) then Wh (8 x 64, rows 6, 7 zero; padded
+// to the 16 MFMA rows) as hi, mid and lo bf16 pieces (each the bf16, round to nearest, of the
+// remainder in double) in the lanes' operand order: W2 [piece][nt][kb][l16][q][e] at 0, Wh
+// [piece][kb][l16][q][e] at 3 * 4096; element e of lane (l16, q) is column 32 kb + 4q + (e < 4 ? e :
+// 12 + e) of row 16 nt + l16 (Wh: row l16).
+void decoder_x3_weights(const float* w2, const float* wh, uint16_t* out) {
+  auto put = [&](double r, size_t i0, size_t stride) {
+    for (int pc = 0; pc < 3; ++pc) {
+      float f = (float)r;
+      uint32_t u;
+      memcpy(&u, &f, 4);
+      const uint16_t b = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+      const uint32_t ub = (uint32_t)b << 16;
+      float fb;
+      memcpy(&fb, &ub, 4);
+      out[i0 + pc * stride] = b;
+      r -= fb;
+    }
+  };
+  for (int nt = 0; nt < 4; ++nt)
+    for (int kb = 0; kb < 2; ++kb)
+      for (int l = 0; l < 16; ++l)
+        for (int q = 0; q < 4; ++q)
+          for (int e = 0; e < 8; ++e)
+            put(w2[(16 * nt + l) * 64 + 32 * kb + 4 * q + (e < 4 ? e : 12 + e)],
+                ((((size_t)nt * 2 + kb) * 16 + l) * 4 + q) * 8 + e, 4096);
+  for (int kb = 0; kb < 2; ++kb)
+    for (int l = 0; l < 16; ++l)
+      for (int q = 0; q < 4; ++q)
+        for (int e = 0; e < 8; ++e)
+          put(l < 8 ? wh[l * 64 + 32 * kb + 4 * q + (e < 4 ? e : 12 + e)] : 0.0,
+              3 * 4096 + (((size_t)kb * 16 + l) * 4 + q) * 8 + e, 1024);
+}
+
 hipError_t launch_decoder(const DecParams& p, hipStream_t s) {
-  if (p.x3 && !p.w2x3) return hipErrorInvalidValue;
+  if ((p.x3 || p.bf16) && !p.w2x3) return hipErrorInvalidValue;  // the split-bf16 heads' Wh pieces
   return launch_dec(p, s, p.bf16 ? 1 : p.x3 ? 4 : 0);
 }
 

@@ -791,31 +791,16 @@ int clasfv_finalize(clasfv_t h) {
     (void)hipFree(*d);
     *d = nullptr;
   }
-  // W2 = hi + mid + lo, each piece the bf16 of the remainder (exact in double), in the lane order of the
-  // decoder's comb_2 B operand: [piece][nt][kb][l16][q][e], element e of lane (l16, q) = W2[16nt + l16]
-  // [32kb + 4q + (e < 4 ? e : 12 + e)] (decoder.hip, decoder_heads_bf16<true>)
-  std::vector<float> w2x3(3 * 64 * 64);
-  for (int nt = 0; nt < 4; ++nt)
-    for (int kb = 0; kb < 2; ++kb)
-      for (int l = 0; l < 16; ++l)
-        for (int q = 0; q < 4; ++q)
-          for (int e = 0; e < 8; ++e) {
-            const size_t i = ((((size_t)nt * 2 + kb) * 16 + l) * 4 + q) * 8 + e;
-            double r = w2f[(16 * nt + l) * 64 + 32 * kb + 4 * q + (e < 4 ? e : 12 + e)];
-            for (int pc = 0; pc < 3; ++pc) {
-              const uint16_t b = to_bf16((float)r);
-              uint32_t u = (uint32_t)b << 16;
-              float f;
-              memcpy(&f, &u, 4);
-              w2x3[(size_t)pc * 4096 + i] = f;
-              r -= f;
-            }
-          }
+  // W2 and the head weights as hi + mid + lo bf16 pieces in the X3 decoder's lane order
+  std::vector<uint16_t> w2x3(DECODER_X3_ELEMS);
+  decoder_x3_weights(w2f.data(), whf.data(), w2x3.data());
   (void)hipFree(h->w2x3);
   h->w2x3 = nullptr;
   int rc = upload(b1, &h->b1);
   if (!rc) rc = upload(w2f, &h->w2);
-  if (!rc) rc = upload_bf16(w2x3, &h->w2x3);
+  if (!rc && hipMalloc(&h->w2x3, w2x3.size() * sizeof(uint16_t)) != hipSuccess) rc = fail(CLASFV_EHIP, "hipMalloc");
+  if (!rc && hipMemcpy(h->w2x3, w2x3.data(), w2x3.size() * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess)
+    rc = fail(CLASFV_EHIP, "hipMemcpy");
   if (!rc) rc = upload(b2, &h->b2);
   if (!rc) rc = upload(whf, &h->wh);
   if (!rc) rc = upload(bhf, &h->bh);

@@ -254,37 +254,17 @@ static int run_decoder(int N, int T, int H, int W, int iters, const std::vector<
   CK(hipMalloc((void**)&d.mot, (size_t)N * 4 * T * H * W * 4));
   d.N = N, d.T = T, d.H = H, d.W = W;
   d.bf16 = getenv("CB_BF16") ? 1 : 0;
-  if (getenv("CB_X3")) {  // the fp32 engines' split-bf16 comb_2: W2's hi/mid/lo pieces in lane order
-    std::vector<float> w2(64 * 64), x3(3 * 64 * 64);
+  if (getenv("CB_X3") || d.bf16) {  // split-bf16 comb_2 (X3) and heads: W2 / Wh pieces in lane order
+    std::vector<float> w2(64 * 64), wh(8 * 64);
     CK(hipMemcpy(w2.data(), d.w2, w2.size() * 4, hipMemcpyDeviceToHost));
-    for (int nt = 0; nt < 4; ++nt)
-      for (int kb = 0; kb < 2; ++kb)
-        for (int l = 0; l < 16; ++l)
-          for (int q = 0; q < 4; ++q)
-            for (int e = 0; e < 8; ++e) {
-              const size_t i = ((((size_t)nt * 2 + kb) * 16 + l) * 4 + q) * 8 + e;
-              double r = w2[(16 * nt + l) * 64 + 32 * kb + 4 * q + (e < 4 ? e : 12 + e)];
-              for (int pc = 0; pc < 3; ++pc) {
-                float f = (float)r;
-                uint32_t u;
-                memcpy(&u, &f, 4);
-                u = (u + 0x7fff + ((u >> 16) & 1)) & 0xffff0000u;
-                memcpy(&f, &u, 4);
-                x3[(size_t)pc * 4096 + i] = f;
-                r -= f;
-              }
-            }
-    std::vector<uint16_t> xb(x3.size());
-    for (size_t i = 0; i < x3.size(); ++i) {
-      uint32_t u;
-      memcpy(&u, &x3[i], 4);
-      xb[i] = (uint16_t)(u >> 16);
-    }
+    CK(hipMemcpy(wh.data(), d.wh, wh.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<uint16_t> xb(DECODER_X3_ELEMS);
+    decoder_x3_weights(w2.data(), wh.data(), xb.data());
     void* dx;
     CK(hipMalloc(&dx, xb.size() * 2));
     CK(hipMemcpy(dx, xb.data(), xb.size() * 2, hipMemcpyHostToDevice));
     d.w2x3 = dx;
-    d.x3 = 1;
+    d.x3 = getenv("CB_X3") ? 1 : 0;
   }
   hipStream_t s;
   CK(hipStreamCreate(&s));
