@@ -392,6 +392,10 @@ ConvParams conv_params(const Conv& c, const Shape5& in, Shape5& out) {
 
 // The kernel run_conv launches for c with parameters p (p.vflags selects A/B variants).
 const char* pick_kernel(const Conv& c, ConvParams p) {
+  // 7x7 maps (layer4 at 112x112 clips): the split-bf16 direct GEMM beats F(4x4)'s partial edge tiles
+  // (convbench 0.284 vs 0.312 ms per 1152-channel launch, profiles/r03p_dma_x3_tiles.txt); per-clip
+  // shape rule
+  if (c.dwino4 && c.dx3 && p.Ho * p.Wo <= 64 && !p.y_c8 && dma_x3_supported(p)) return "conv_dma_x3";
   if (c.dwino4 && !(p.vflags & CLASFV_VARIANT_NO_WINO4) && wino4_supported(p)) return "conv_wino4";
   if (c.dwino) {
     const bool no_patch = (p.vflags & CLASFV_VARIANT_NO_WINO_PATCH) != 0;
