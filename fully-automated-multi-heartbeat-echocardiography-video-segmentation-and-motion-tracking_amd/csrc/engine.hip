@@ -404,6 +404,10 @@ const char* pick_kernel(const Conv& c, ConvParams p) {
   }
   if (c.dws16 && !(p.vflags & CLASFV_VARIANT_NO_STEM_BF16) && stem_bf16_supported(p)) return "conv_stem_bf16";
   if (c.dws16 && stem_x3_supported(p)) return "conv_stem_x3";
+  // temporal convs on <= 256-voxel clip maps (layer4, T = 4): split-K 4 on the split-bf16 direct GEMM
+  // beats the one-tile-row F(4,3) form (convbench 0.119 vs 0.145 ms with both split sums)
+  if (c.dwinot && c.dx3 && (long)p.To * p.Ho * p.Wo <= 256 && !p.x_c8 && !p.y_c8 && dma_x3_supported(p))
+    return "conv_dma_x3";
   if (c.dwinot && winot_supported(p)) return "conv_winot";
   if (!(p.vflags & CLASFV_VARIANT_NO_PATCH_BF16) && patch_bf16_supported(p)) return "conv_patch_bf16";
   if (c.dx3 && dma_x3_supported(p)) return "conv_dma_x3";
