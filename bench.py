@@ -188,7 +188,10 @@ def profiled_traffic(kernel, dtype):
     tools/prof_summary.py, FETCH already x2-corrected (MI355X_MICROARCH.md HBM section)."""
     import glob
     import re
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_traffic_{dtype}.txt")))
+    def tag(path):  # r<round><letters>_...: round, then a..z, aa..zz (profile series order)
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_traffic_{dtype}.txt")), key=tag)
     if not files:
         return None
     m = re.search(r"^pmc %s launches=(\d+) fetch_mib=([\d.]+) write_mib=([\d.]+)" % re.escape(kernel),
