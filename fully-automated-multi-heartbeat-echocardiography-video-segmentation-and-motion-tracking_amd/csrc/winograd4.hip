@@ -375,6 +375,42 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
       }
     }
     __syncthreads();
+    if constexpr ((KO & 32768) != 0) {
+      // probe (correct results): unit = (channel, column b, 4 tiles) -- 16-B plane reads over 4 tiles
+      // instead of 4-B reads over 4 channels, one 4-B store per (tile, row)
+      const int c16 = tid & 15, vb = (tid >> 4) & 3, tg = tid >> 6;
+      const int veb = vb == 3 ? 1 : vb;
+      f32x4 P[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+        P[i] = *reinterpret_cast<const f32x4*>(Z + (i * 3 + veb) * W4_ZS + c16 * W4_CS + 4 * tg) +
+               *reinterpret_cast<const f32x4*>(Z + (18 + i * 4 + vb) * W4_ZS + c16 * W4_CS + 4 * tg);
+      const int co = cob * 48 + nt * 16 + c16;
+      const float bias = p.bias ? p.bias[co] : 0.f;
+      const f32x4 s12 = P[1] + P[2], d12 = P[1] - P[2], s34 = P[3] + P[4], d34 = P[3] - P[4];
+      f32x4 y[4];
+      y[0] = P[0] + s12 + s34;
+      y[1] = d12 + 2.f * d34;
+      y[2] = s12 + 4.f * s34;
+      y[3] = d12 + 8.f * d34 + P[5];
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const int tile = 4 * tg + tt;
+        const int vseg = fdiv(tile, g.fd_tc), vtc = tile - vseg * g.TC;
+        const int vR = R0 + vseg, vf = fdiv(vR, g.fd_th), vty = vR - vf * g.TH;
+        const int vxx = 4 * (tx0 + vtc) + vb;
+        if (tile >= NT || vxx >= W) continue;
+#pragma unroll
+        for (int aa = 0; aa < 4; ++aa) {
+          if (4 * vty + aa >= H) break;
+          float o = y[aa][tt] + bias;
+          if constexpr (RELU) o = fmaxf(o, 0.f);
+          const size_t pix = (size_t)(vf * H + 4 * vty + aa) * W + vxx;
+          yout[C8 ? (size_t)(co >> 3) * plane + pix * 8 + (co & 7) : pix * CO + co] = o;
+        }
+      }
+      continue;
+    }
     if (ulive) {
       f32x4 P[6];
       const int eb = ub == 3 ? 1 : ub;
@@ -383,7 +419,12 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         const float* e = Z + (i * 3 + eb) * W4_ZS + (4 * ucq) * W4_CS + utile;
         const float* f = Z + (18 + i * 4 + ub) * W4_ZS + (4 * ucq) * W4_CS + utile;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) P[i][c] = e[c * W4_CS] + f[c * W4_CS];
+        for (int c = 0; c < 4; ++c) {
+          if constexpr ((KO & 16384) != 0)  // probe: no unit LDS reads
+            P[i][c] = (float)(i + c + utile);
+          else
+            P[i][c] = e[c * W4_CS] + f[c * W4_CS];
+        }
       }
       const int co = cob * 48 + nt * 16 + 4 * ucq;
       const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -403,7 +444,13 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         }
         const size_t pix = (size_t)(uf * H + 4 * uty + aa) * W + uxx;
         const size_t off = C8 ? (size_t)(co >> 3) * plane + pix * 8 + (co & 7) : pix * CO + co;
-        *reinterpret_cast<f32x4*>(yout + off) = o;
+        if constexpr ((KO & 8192) != 0) {  // probe: no output stores
+          if (o[0] == 1234.5f) *reinterpret_cast<f32x4*>(yout + off) = o;
+        } else if constexpr ((KO & 65536) != 0) {  // probe: non-temporal output stores
+          __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(yout + off));
+        } else {
+          *reinterpret_cast<f32x4*>(yout + off) = o;
+        }
       }
     }
   }
@@ -577,6 +624,11 @@ hipError_t launch_wino4_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 192: return launch_w4ko<192>(p, g, nb, s);
     case 256: return launch_w4ko<256>(p, g, nb, s);
     case 4096: return launch_w4ko<4096>(p, g, nb, s);
+    case 8192: return launch_w4ko<8192>(p, g, nb, s);
+    case 16384: return launch_w4ko<16384>(p, g, nb, s);
+    case 24576: return launch_w4ko<24576>(p, g, nb, s);
+    case 32768: return launch_w4ko<32768>(p, g, nb, s);
+    case 65536: return launch_w4ko<65536>(p, g, nb, s);
     default: return launch_w4ko<0>(p, g, nb, s);
   }
 }
