@@ -482,10 +482,11 @@ def run_c1(args, model, world, rank, dev):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "dtype_note": ("fp32 activations, weights and accumulation; Winograd / stem convs on f32 MFMAs, "
-                       "strided / 1x1x1 convs, projections and comb_2 on split-bf16 MFMAs (3 bf16 pieces "
-                       "per operand, 6 products, fp32 accumulation: fp32-accurate; variants no_dma_x3 / "
-                       "no_decoder_x3 run them on f32 MFMAs)") if args.dtype == "fp32" else None,
+        "dtype_note": ("fp32 activations, weights and accumulation; the Winograd convs (layer1-3) on f32 "
+                       "MFMAs; the stem, strided / 1x1x1 convs, layer4 convs, decoder projections, comb_2 "
+                       "and heads on split-bf16 MFMAs (3 bf16 pieces per operand, 6 products, fp32 "
+                       "accumulation: fp32-accurate; variants no_stem_x3 / no_dma_x3 / no_decoder_x3 run "
+                       "them on f32 MFMAs)") if args.dtype == "fp32" else None,
         "data": "synthetic EchoNet-style video (seeded), seeded synthetic weights (" + BENCH_WEIGHTS + " recipe)",
         "config": {"workload": "BASELINE config[1] per GPU: 200-frame 112x112 video, 5 shifted passes "
                                "(30 x 32-frame clips) + per-frame SIMPLE label fusion",
