@@ -394,29 +394,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       d[ND - 1] = f32x2{0.f, 0.f};
       if constexpr (COLS) d[5] = f32x2{0.f, 0.f};
     }
-    f32x2 v[2][6];
-    if constexpr ((EPI & 256) != 0) {
+    // B^T row e of tile m, formed right before its MFMAs (the 12 transformed values of both tiles
+    // held at once, beside the 192-register accumulator, spilled at NT = 4); the same expressions
+    // as the reference kernel, per element
+    auto vrow = [&](int m, int e) __attribute__((always_inline)) {
+      f32x2 r;
+      if constexpr ((EPI & 256) != 0) {
+        r = d[MS * m + e];
+      } else {
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int e = 0; e < 6; ++e) v[m][e] = d[MS * m + e];
-    } else
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const float d0 = d[MS * m][s2], d1 = d[MS * m + 1][s2], d2 = d[MS * m + 2][s2], d3 = d[MS * m + 3][s2],
-                    d4 = d[MS * m + 4][s2], d5 = d[MS * m + 5][s2];
-        const float e1 = d3 + d4, e2 = d1 + d2, e3 = d4 - d3, e4 = d1 - d2;
-        v[m][0][s2] = 4.f * d0 - 5.f * d2 + d4;
-        v[m][1][s2] = e1 - 4.f * e2;
-        v[m][2][s2] = e3 + 4.f * e4;
-        v[m][3][s2] = (d4 - d2) + 2.f * (d3 - d1);
-        v[m][4][s2] = (d4 - d2) - 2.f * (d3 - d1);
-        v[m][5][s2] = 4.f * d1 - 5.f * d3 + d5;
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const float d0 = d[MS * m][s2], d1 = d[MS * m + 1][s2], d2 = d[MS * m + 2][s2], d3 = d[MS * m + 3][s2],
+                      d4 = d[MS * m + 4][s2], d5 = d[MS * m + 5][s2];
+          float x;
+          if (e == 0) x = 4.f * d0 - 5.f * d2 + d4;
+          else if (e == 1) { const float e1 = d3 + d4, e2 = d1 + d2; x = e1 - 4.f * e2; }
+          else if (e == 2) { const float e3 = d4 - d3, e4 = d1 - d2; x = e3 + 4.f * e4; }
+          else if (e == 3) x = (d4 - d2) + 2.f * (d3 - d1);
+          else if (e == 4) x = (d4 - d2) - 2.f * (d3 - d1);
+          else x = 4.f * d1 - 5.f * d3 + d5;
+          r[s2] = x;
+        }
       }
+      return r;
+    };
 #pragma unroll
     for (int e = 0; e < 6; ++e) {
+      f32x2 v[2][6];
+      v[0][e] = vrow(0, e);
+      v[1][e] = vrow(1, e);
       f32x2 u[NT];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) u[nt] = *reinterpret_cast<const f32x2*>(st + u_rd + (e * G::CB + nt * 16) * 8);
