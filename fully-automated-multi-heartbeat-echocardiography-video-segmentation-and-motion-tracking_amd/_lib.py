@@ -14,6 +14,7 @@ _P = c_void_p
 SIGNATURES = {
     "clasfv_last_error": (c_char_p, []),
     "clasfv_version": (c_int, []),
+    "clasfv_source_hash": (c_char_p, []),
     "clasfv_create": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
     "clasfv_destroy": (c_int, [_P]),
     "clasfv_param_count": (c_int, [_P]),
@@ -58,13 +59,22 @@ def lib_path():
 
 
 def load():
-    """Load (building first if needed) and return the ctypes library."""
+    """Load and return the ctypes library. A library whose embedded source hash differs from the
+    sources on disk (older than them, or built from other ones) is rebuilt before it is loaded --
+    never used stale; without hipcc that rebuild raises."""
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        from .build import build
-        build()
+    from . import build as B
+    want = B.source_hash()
+    have = B.library_hash()
+    if have != want:
+        import sys
+        print(f"clasfv: {LIB_PATH} {'missing' if have is None and not os.path.exists(LIB_PATH) else 'stale'} "
+              f"(library source hash {have}, sources {want}): rebuilding", file=sys.stderr)
+        B.build(force=B.library_hash() != want)
+        if B.library_hash() != want:
+            raise RuntimeError(f"{LIB_PATH}: rebuild did not produce a library of the current sources")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
@@ -73,6 +83,9 @@ def load():
     if lib.clasfv_version() != ABI_VERSION:
         raise RuntimeError(f"{LIB_PATH}: ABI version {lib.clasfv_version()}, expected {ABI_VERSION}: rebuild it "
                            f"(python -m clasfv_amd.build --force)")
+    got = lib.clasfv_source_hash().decode()
+    if got != B.HASH_MARK.decode() + want:
+        raise RuntimeError(f"{LIB_PATH}: loaded library reports {got}, sources hash to {want}")
     _lib = lib
     return lib
 

@@ -1,9 +1,14 @@
 """Build ``libclasfv.so`` (all HIP kernels + the C ABI) for gfx950 with hipcc, in-tree.
 
 The shared library lands next to this file so it travels with the repository snapshot to the GPU
-box (a JIT cache under ~/.cache would not). Rebuilt only when a source is newer than the library.
+box (a JIT cache under ~/.cache would not). The build embeds a content hash of its sources
+(``clasfv_source_hash()``); the library counts as up to date only when that hash equals the hash of
+the sources on disk, so a prebuilt binary older than its sources is never used (file times are not
+trusted: a snapshot can carry any mtime).
 """
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -35,11 +40,33 @@ def _inputs():
     return files
 
 
+HASH_MARK = b"clasfv-source-hash:"
+
+
+def source_hash():
+    """16 hex digits of SHA-256 over the names and bytes of every build input, the compile flags
+    included (what clasfv_source_hash() of a library built from them returns after the mark)."""
+    h = hashlib.sha256()
+    h.update(repr((ARCH, sorted(EXTRA_FLAGS.items()))).encode())
+    for f in _inputs():
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def library_hash(path=LIB_PATH):
+    """The source hash embedded in a built library (read from its bytes, without loading it), or
+    None when the file is missing or carries no hash."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as fh:
+        m = re.search(re.escape(HASH_MARK) + rb"([0-9a-f]{16})", fh.read())
+    return m.group(1).decode() if m else None
+
+
 def up_to_date():
-    if not os.path.exists(LIB_PATH):
-        return False
-    t = os.path.getmtime(LIB_PATH)
-    return all(os.path.getmtime(f) <= t for f in _inputs())
+    return library_hash() == source_hash()
 
 
 def build(force=False, verbose=False):
@@ -67,10 +94,14 @@ def _build_locked(verbose):
     objdir = tempfile.mkdtemp(prefix="build-", dir=os.path.join(PKG_DIR, "build_obj"))
     hipcc = _hipcc()
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", INCLUDE]
+    digest = source_hash()
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
-        cmd = [hipcc] + flags + EXTRA_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+        extra = list(EXTRA_FLAGS.get(src, []))
+        if src == "engine.hip":
+            extra.append(f'-DCLASFV_SOURCE_HASH="{digest}"')
+        cmd = [hipcc] + flags + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True)

@@ -584,6 +584,10 @@ extern "C" {
 
 const char* clasfv_last_error(void) { return g_err.c_str(); }
 int clasfv_version(void) { return CLASFV_ABI_VERSION; }
+#ifndef CLASFV_SOURCE_HASH
+#define CLASFV_SOURCE_HASH "unhashed"
+#endif
+const char* clasfv_source_hash(void) { return "clasfv-source-hash:" CLASFV_SOURCE_HASH; }
 
 int clasfv_create(int device, clasfv_t* out) {
   if (!out) return fail(CLASFV_EINVAL, "null out");
@@ -881,10 +885,28 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
     HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
   }
-  // a decoder projection on the side stream once its tap is complete on s (timed with its own events)
+  // Once work is forked to the side stream, every exit of this call (the error returns included)
+  // leaves s ordered after everything queued there, so the caller's next use of the arena or the
+  // outputs cannot race the projections.
+  struct SideJoin {
+    clasfv_engine* h;
+    hipStream_t s;
+    bool pending = false;
+    hipError_t join() {
+      if (!pending) return hipSuccess;
+      pending = false;
+      hipError_t e = hipEventRecord(h->ev_join, h->side);
+      return e != hipSuccess ? e : hipStreamWaitEvent(s, h->ev_join, 0);
+    }
+    ~SideJoin() { (void)join(); }
+  } side_join{h, s};
+  // a decoder projection on the side stream once its tap is complete on s (timed with its own events;
+  // with kernel timing on, the layer4 launches on s run concurrently with these, so their event
+  // intervals overlap: the per-kernel sums of a forward exceed its wall time by about the overlap)
   auto run_side = [&](const Conv& c, const void* xin, const Shape5& in, void* y, Shape5& out, const void* x2) {
     HIP_TRY(hipEventRecord(h->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    side_join.pending = true;
     const int e0 = h->ktime ? tick(h, h->side) : -1;
     const char* kname = "";
     int rc_ = run_conv(c, xin, in, y, out, nullptr, false, h->side, h->zero, x2, &kname, h->tune);
@@ -892,7 +914,6 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
       const int e1 = tick(h, h->side);
       if (e1 >= 0) h->recs.push_back({kname, conv_gflop(c, out), conv_exec_gflop(c, out, kname), e0, e1});
     }
-    if (!rc_) HIP_TRY(hipEventRecord(h->ev_join, h->side));
     return rc_;
   };
   auto run = [&](const Conv& c, const void* xin, const Shape5& in, void* y, Shape5& out, const void* res, bool relu,
@@ -965,7 +986,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
     }
   }
   if ((rc = run(h->proj[4], taps[4], taps_shape[4], buf(PP4), sp4, nullptr, false))) return rc;
-  HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));  // the side stream's projections are complete
+  HIP_TRY(side_join.join());  // the side stream's projections are complete before the decoder
 
   DecParams d{};
   const Shape5 tsh[4] = {sp, sp2, sp3, sp4};

@@ -482,9 +482,11 @@ bool wino4_geometry(const ConvParams& p, W4Geo* g, int* n_blocks) {
   int TC = 0;
   for (int d = TW < 16 ? TW : 16; d >= 1 && !TC; --d)
     if (TW % d == 0) TC = d;
+  // TR divides one clip's tile rows (To * TH), not the batch's: the group shape -- and so whether this
+  // kernel runs at all, and every clip's rounding -- depends on the per-clip shape only, never on N
   int TR = 0;
   for (int d = 16 / TC; d >= 1 && !TR; --d)
-    if (rows % d == 0) TR = d;
+    if (((long)p.To * TH) % d == 0) TR = d;
   if (TR * TC < 12) return false;
   const int PC = 4 * TC + 2, rp0 = (PC - 1) + (PC - 1) / 4 + 1;
   // RP, SS: fewest tiles sharing a 16-B bank quad of a 256-B row (ds_read_b64: a 32-lane group = 16

@@ -42,10 +42,11 @@ def global_clip_plan(video_lengths, num_clips, step, interpolate_last=True):
     return plans, off
 
 
-def all_gather_clips(local, n_total, rank, world, group=None):
+def all_gather_clips(local, n_total, rank, world, group=None, force=False):
     """Gather per-clip tensors (n_local, ...) from every rank into (n_total, ...) in global order.
-    Blocks are padded to the largest shard so one all_gather_into_tensor moves everything."""
-    if world == 1:
+    Blocks are padded to the largest shard so one all_gather_into_tensor moves everything.
+    ``force``: run the collective even on one rank (tests drive RCCL with a world-size-1 group)."""
+    if world == 1 and not force:
         return local
     sizes = [shard_bounds(n_total, r, world) for r in range(world)]
     mx = max(hi - lo for lo, hi in sizes)
@@ -113,15 +114,16 @@ def rows_exchanged(owners, world):
     return sum(c[s_][o] for s_ in range(world) for o in range(world) if s_ != o)
 
 
-def exchange_to_owners(local, owners, rank, world, group=None):
+def exchange_to_owners(local, owners, rank, world, group=None, force=False):
     """Route per-clip rows to their owners. ``local`` holds rows [lo, hi) of the global clip list
     (this rank's shard_bounds block); ``owners[g]`` is the owner rank of global clip g. Returns the
     rows of every clip this rank owns, in global clip order. One all_to_all_single; skipped when no
-    clip is computed away from its owner (all ranks derive that from the same plan)."""
+    clip is computed away from its owner (all ranks derive that from the same plan) unless ``force``
+    (tests drive RCCL with a world-size-1 group)."""
     n_total = len(owners)
     counts = exchange_counts(owners, world)
     lo, hi = shard_bounds(n_total, rank, world)
-    if world == 1 or rows_exchanged(owners, world) == 0:
+    if not force and (world == 1 or rows_exchanged(owners, world) == 0):
         keep = [g - lo for g in range(lo, hi) if owners[g] == rank]
         if len(keep) == hi - lo:
             return local
@@ -153,13 +155,14 @@ def exchange_stats(lengths, num_clips, step, world, h=112, w=112, interpolate_la
 
 
 def segment_videos_sharded(videos_dev, model, num_clips=5, step=1, fuse_method="simple", interpolate_last=True,
-                           rank=0, world=1, batch_size=None, clip_fn=None, lengths=None):
+                           rank=0, world=1, batch_size=None, clip_fn=None, lengths=None, force_exchange=False):
     """Fuse a batch of device videos (each (3,T,H,W)) with clips sharded over ranks.
 
     Returns {video index: fused (T',H,W) uint8 device tensor} for the videos this rank owns
     (video_owners). ``clip_fn(clips) -> logits`` overrides the model call. With ``lengths`` (the
     frame count of every video) ``videos_dev`` may hold None for videos outside this rank's block
-    (``videos_needed``)."""
+    (``videos_needed``). ``force_exchange``: ship logit margins through the all_to_all even when no
+    clip crosses ranks (tests; the result is the same)."""
     if lengths is None:
         lengths = [v.shape[1] for v in videos_dev]
     plans, n_total = global_clip_plan(list(lengths), num_clips, step, interpolate_last)
@@ -185,10 +188,10 @@ def segment_videos_sharded(videos_dev, model, num_clips=5, step=1, fuse_method="
     lo, hi = shard_bounds(n_total, rank, world)
     local = compute(lo, hi) if hi > lo else empty
     owners = owner_of_clips(plans, world)
-    margin = world > 1 and rows_exchanged(owners, world) > 0
+    margin = force_exchange or (world > 1 and rows_exchanged(owners, world) > 0)
     if margin:  # ship one fp32 plane per clip frame instead of two (bit-identical labels, see above)
         local = FU.logit_margin(local) if local.shape[0] else local[:, 0]
-    mine = exchange_to_owners(local.contiguous(), owners, rank, world)
+    mine = exchange_to_owners(local.contiguous(), owners, rank, world, force=force_exchange)
     vown = video_owners(plans, world)
     out, at = {}, 0
     for vi, p in enumerate(plans):

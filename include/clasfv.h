@@ -81,6 +81,10 @@ typedef struct clasfv_engine* clasfv_t;
 const char* clasfv_last_error(void);
 /* CLASFV_ABI_VERSION of the loaded library. */
 int clasfv_version(void);
+/* Content hash of the sources the library was compiled from ("clasfv-source-hash:<16 hex>",
+ * computed by the build over csrc/ and this header): a binding can refuse a library older than its
+ * sources without trusting file times. Does not change the ABI revision (a new export only). */
+const char* clasfv_source_hash(void);
 
 /* ---- model: replaces R2plus1D_18_MotionNet.__init__/load_state_dict/forward ------------------ */
 int clasfv_create(int device, clasfv_t* out);

@@ -1,9 +1,15 @@
-"""Generate tests/golden/northstar_c1.npz: the CPU reference path at BASELINE config[1].
+"""Generate tests/golden/northstar_c1.npz (and northstar_c1_random.npz): the CPU reference path at
+BASELINE config[1].
 
 One 200-frame synthetic EchoNet-style video (synthetic.echo_video(200, seed=0), zero-one normalised),
-5 temporally shifted passes with step 1 (30 clips of 32 frames), the seeded "echo" weights
-(weights.echo_state_dict(DEFAULT_SEED): the segmentation follows the synthetic LV, so the EFs are
-physiological, ~76 %) -- exactly bench.py's per-GPU workload. Everything is
+5 temporally shifted passes with step 1 (30 clips of 32 frames) -- exactly bench.py's per-GPU
+workload -- with one of two seeded weight recipes:
+  echo    (northstar_c1.npz)        weights.echo_state_dict(DEFAULT_SEED): the segmentation follows
+          the synthetic LV, so the EFs are physiological (~77 %); the LV decision runs through the
+          stem, layer1 and the decoder (layer2-4 reach the logits at ~1e-2 of the margin);
+  random  (northstar_c1_random.npz) weights.synthetic_state_dict(DEFAULT_SEED): every layer at full
+          gain, so every conv of the encoder moves the fused masks (EFs degenerate).
+Everything is
 computed by the oracle (tests-only infrastructure): the torch-CPU restatement of the reference model
 (oracle/r2plus1d_ref.py, pinned to the reference module by tests/golden/model_forward.npz) and the
 numpy restatement of src/fuse_utils.py (oracle/fuse_ref.py, pinned by tests/golden/plumbing.npz).
@@ -14,7 +20,8 @@ Stored (bit-packed masks):
   ef_<method>     compute_ef_using_putative_clips of each fused mask (EF list and ED/ES pairs)
   logit_margin_*  |l1 - l0| statistics, to tell how close the fused masks are to argmax ties
 
-Run in the build container: python tests/golden/make_golden_northstar.py (about a minute).
+Run in the build container: python tests/golden/make_golden_northstar.py [echo|random] (about a
+minute each).
 """
 import os
 import sys
@@ -30,7 +37,8 @@ sys.path.insert(0, REPO)
 from oracle import fuse_ref, r2plus1d_ref  # noqa: E402
 
 T, F, STEP, SEED = 200, 5, 1, 0
-RECIPE = "echo"
+RECIPE = sys.argv[1] if len(sys.argv) > 1 else "echo"
+OUT = {"echo": "northstar_c1.npz", "random": "northstar_c1_random.npz"}[RECIPE]
 METHODS = ("majority", "simple", "staple")
 
 
@@ -69,7 +77,7 @@ def main():
         out[f"ef_{meth}"] = np.array(efs, np.float64)
         out[f"pairs_{meth}"] = np.array(pairs, np.int64).reshape(-1, 2)
         print(meth, "LV fraction", float(fused.mean()), "EF", np.round(efs, 3), "pairs", pairs)
-    np.savez_compressed(os.path.join(HERE, "northstar_c1.npz"), **out)
+    np.savez_compressed(os.path.join(HERE, OUT), **out)
 
 
 if __name__ == "__main__":
