@@ -102,6 +102,13 @@ double wino4_exec_gflop(const ConvParams& p);
 // w[cout][cin][3][3] (double).
 void wino4_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 size_t wino4_weight_floats(int cin_p, int cout_p);
+// conv_wino4 with wide output-channel blocks (16 NTN channels, NTN = wino4w_ntn(cout) in {9, 6, 5}; one
+// 4-wave block per CU; winograd4w.hip): the same products and order as conv_wino4, bit-identical.
+bool wino4w_supported(const ConvParams& p);
+hipError_t launch_wino4w(const ConvParams& p, hipStream_t s);
+double wino4w_exec_gflop(const ConvParams& p);
+void wino4w_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
+size_t wino4w_weight_floats(int cin_p, int cout_p);  // 0: no wide block for this cout_p
 // Fused Winograd F(4,3)-in-time path for stride-1 3x1x1 fp32 convs; p.w = transformed weights.
 bool winot_supported(const ConvParams& p);
 hipError_t launch_winot(const ConvParams& p, hipStream_t s);

@@ -79,6 +79,7 @@ struct Conv {
   float* db = nullptr;    // folded-BN bias (fp32)
   float* dwino = nullptr;  // Winograd F(2x2,3x3) transformed weights (fp32 stride-1 1x3x3 convs)
   float* dwino4 = nullptr;  // Winograd F(4x4,3x3) transformed weights (the same convs, cout_p % 48 == 0)
+  float* dwino4w = nullptr;  // the same for conv_wino4w's wide output-channel blocks (wino4w_ntn(cout_p) > 0)
   float* dwinot = nullptr;  // Winograd F(4,3)-in-time transformed weights (fp32 stride-1 3x1x1 convs)
   void* dws16 = nullptr;    // bf16 stem weights, hi and lo images [64][7 kh][8 kw][4 c] (bf16 engines);
                             // fp32 engines: hi, mid and lo images [48][7][8][4] (conv_stem_x3)
@@ -118,6 +119,7 @@ int env_variants() {
   if (on("CLASFV_NO_DECODER_X3")) f |= CLASFV_VARIANT_NO_DECODER_X3;
   if (on("CLASFV_NO_DMA_X3")) f |= CLASFV_VARIANT_NO_DMA_X3;
   if (on("CLASFV_NO_STEM_X3")) f |= CLASFV_VARIANT_NO_STEM_X3;
+  if (on("CLASFV_NO_WINO4W")) f |= CLASFV_VARIANT_NO_WINO4W;
   return f;
 }
 
@@ -341,11 +343,11 @@ double conv_gflop(const Conv& c, const Shape5& out) {
 double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
   const double nt = (double)out.n * out.t;
   const double cc = (double)c.cin_p * c.cout_p;
-  if (!strcmp(kname, "conv_wino4")) {  // F(4x4,3x3): 36 products per 4x4 tile and channel pair, 16-tile groups
-    ConvParams p{};
+  if (!strcmp(kname, "conv_wino4") || !strcmp(kname, "conv_wino4w")) {  // F(4x4,3x3): 36 products per 4x4
+    ConvParams p{};                                                           // tile and channel pair, 16-tile groups
     p.N = out.n, p.Ti = p.To = out.t, p.Hi = p.Ho = out.h, p.Wi = p.Wo = out.w;
     p.Cin = c.cin_p, p.Cout = c.cout_p;
-    return wino4_exec_gflop(p);
+    return kname[10] == 'w' ? wino4w_exec_gflop(p) : wino4_exec_gflop(p);
   }
   if (!strcmp(kname, "conv_wino_q") || !strcmp(kname, "conv_wino"))
     return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 1) / 2) * 16.0 * cc * 1e-9;
@@ -396,6 +398,8 @@ const char* pick_kernel(const Conv& c, ConvParams p) {
   // (convbench 0.284 vs 0.312 ms per 1152-channel launch, profiles/r03p_dma_x3_tiles.txt); per-clip
   // shape rule
   if (c.dwino4 && c.dx3 && p.Ho * p.Wo <= 64 && !p.y_c8 && dma_x3_supported(p)) return "conv_dma_x3";
+  if (c.dwino4w && !(p.vflags & (CLASFV_VARIANT_NO_WINO4 | CLASFV_VARIANT_NO_WINO4W)) && wino4w_supported(p))
+    return "conv_wino4w";
   if (c.dwino4 && !(p.vflags & CLASFV_VARIANT_NO_WINO4) && wino4_supported(p)) return "conv_wino4";
   if (c.dwino) {
     const bool no_patch = (p.vflags & CLASFV_VARIANT_NO_WINO_PATCH) != 0;
@@ -422,14 +426,15 @@ bool c8_pair(const Conv& a, const Conv& b, const Shape5& in, const Tuning& tu) {
   Shape5 mid, out;
   ConvParams pa = conv_params(a, in, mid);
   ConvParams pb = conv_params(b, mid, out);
-  pa.w = a.dwino4 ? (const void*)a.dwino4 : a.dwino ? (const void*)a.dwino : a.dw;
+  pa.w = a.dwino4w ? (const void*)a.dwino4w : a.dwino4 ? (const void*)a.dwino4 : a.dwino ? (const void*)a.dwino : a.dw;
   pb.w = b.dwinot;
   pa.vflags = pb.vflags = tu.vflags;
   const char* ka = pick_kernel(a, pa);
   // Measured per producer (30 clips, profiles/r02j_*): stem and conv_wino_q (layer1, layer2) write
   // the blocked layout at no cost while the temporal kernels after them gain 7-24 %; conv_wino
   // (layer3) broke even and stays channels-last.
-  const bool writes = !strcmp(ka, "conv_wino4") || !strcmp(ka, "conv_wino_q") || !strcmp(ka, "conv_stem_f32") ||
+  const bool writes = !strcmp(ka, "conv_wino4") || !strcmp(ka, "conv_wino4w") || !strcmp(ka, "conv_wino_q") ||
+                      !strcmp(ka, "conv_stem_f32") ||
                       !strcmp(ka, "conv_stem_x3");
   return writes && !a.out_bf16 && !strcmp(pick_kernel(b, pb), "conv_winot") && winot_c8_ok(pb);
 }
@@ -451,11 +456,15 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   p.y_c8 = y_c8;
   const char* k = pick_kernel(c, p);
   *kname = k;
-  const bool c8_out = !strcmp(k, "conv_wino4") || !strcmp(k, "conv_wino_q") || !strcmp(k, "conv_stem_f32") ||
+  const bool c8_out = !strcmp(k, "conv_wino4") || !strcmp(k, "conv_wino4w") || !strcmp(k, "conv_wino_q") ||
+                      !strcmp(k, "conv_stem_f32") ||
                       !strcmp(k, "conv_stem_x3");
   if ((y_c8 && !c8_out) || (x_c8 && strcmp(k, "conv_winot")))
     return fail(CLASFV_EINVAL, "internal: 8-channel-blocked layout on an unsupported kernel");
-  if (!strcmp(k, "conv_wino4")) {
+  if (!strcmp(k, "conv_wino4w")) {
+    p.w = c.dwino4w;
+    HIP_TRY(launch_wino4w(p, s));
+  } else if (!strcmp(k, "conv_wino4")) {
     p.w = c.dwino4;
     HIP_TRY(launch_wino4(p, s));
   } else if (!strcmp(k, "conv_wino_q")) {
@@ -613,6 +622,7 @@ int clasfv_destroy(clasfv_t h) {
     (void)hipFree(c.db);
     (void)hipFree(c.dwino);
     (void)hipFree(c.dwino4);
+    (void)hipFree(c.dwino4w);
     (void)hipFree(c.dwinot);
     (void)hipFree(c.dws16);
     (void)hipFree(c.dx3);
@@ -683,12 +693,13 @@ int clasfv_finalize(clasfv_t h) {
     (void)hipFree(c.db);
     (void)hipFree(c.dwino);
     (void)hipFree(c.dwino4);
+    (void)hipFree(c.dwino4w);
     (void)hipFree(c.dwinot);
     (void)hipFree(c.dws16);
     (void)hipFree(c.dx3);
     c.dw = c.dws16 = c.dx3 = nullptr;
     c.db = nullptr;
-    c.dwino = c.dwino4 = c.dwinot = nullptr;
+    c.dwino = c.dwino4 = c.dwino4w = c.dwinot = nullptr;
     bn_scale_shift(h, c.bn, c.cout, s, t);
     const auto& w = P(h, c.w + ".weight");
     const int taps = c.kt * c.kh * c.kw;
@@ -707,6 +718,11 @@ int clasfv_finalize(clasfv_t h) {
         std::vector<float> u4(wino4_weight_floats(c.cin_p, c.cout_p));
         wino4_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, u4.data());
         if ((rc = upload(u4, &c.dwino4))) return rc;
+      }
+      if (c.cin_p % 8 == 0 && wino4w_weight_floats(c.cin_p, c.cout_p)) {
+        std::vector<float> uw(wino4w_weight_floats(c.cin_p, c.cout_p));
+        wino4w_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, uw.data());
+        if ((rc = upload(uw, &c.dwino4w))) return rc;
       }
     }
     if (!bf16 && c.stem && c.cout_p == 48 && c.kh == 7 && c.kw == 7 && cin <= 4) {  // conv_stem_x3's pieces
@@ -842,7 +858,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0x1FFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~0x3FFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;

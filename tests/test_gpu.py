@@ -594,6 +594,25 @@ def test_wino4_matches_wino2(model, shape):
     assert np.all(np.abs(d[flips]) <= 2 * SEG_ATOL)
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (3, 3, 24, 32, 32), (2, 3, 16, 64, 48),
+                                   (1, 3, 16, 112, 224)])
+def test_wino4w_bitexact_vs_wino4(model, shape):
+    """conv_wino4w (wide output-channel blocks: 144 / 288 / 576 channels as 144-channel blocks, 240 as
+    80, 480 as 96) issues conv_wino4's products in conv_wino4's order (variant no_wino4w): the forward
+    is bit-identical, with the wide kernel really running."""
+    rng = np.random.default_rng(47)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    model.engine.set_kernel_timing(True)
+    s_w, m_w = model(x)
+    kt = model.engine.kernel_timing()
+    model.engine.set_kernel_timing(False)
+    assert "conv_wino4w" in kt
+    model.set_kernel_variants("no_wino4w")
+    s_4, m_4 = model(x)
+    model.set_kernel_variants()
+    assert torch.equal(s_w, s_4) and torch.equal(m_w, m_4)
+
+
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 8, 32, 48)])
 def test_decoder_x3_matches_fp32_mfma(model, shape):
     """The fp32 engines' comb_2 on six split-bf16 products (hi/mid/lo pieces of both operands, fp32

@@ -19,6 +19,7 @@ hipError_t launch_wino_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winoq_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_wino4_ko(const ConvParams& p, hipStream_t s, int ko);
+hipError_t launch_wino4w_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winor_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_dma_x3_cfg(const ConvParams& p, int mt, int nt, int S, hipStream_t s);
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
@@ -89,7 +90,8 @@ int main(int argc, char** argv) {
   const bool winoqp = !strcmp(kind, "winoqp");  // conv_wino_q knock-out probes (tools/winoq_probe.hip)
   const bool winoq = !strcmp(kind, "winoq") || winoqp, winor = !strcmp(kind, "winor");
   const bool wino4 = !strcmp(kind, "wino4");  // conv_wino4 (F(4x4,3x3); no residual)
-  const bool wino = !strcmp(kind, "wino") || winoq || winor || wino4, winot = !strcmp(kind, "winot");
+  const bool wino4w = !strcmp(kind, "wino4w");  // conv_wino4w (wide blocks; ko: knock-outs at NTN 9)
+  const bool wino = !strcmp(kind, "wino") || winoq || winor || wino4 || wino4w, winot = !strcmp(kind, "winot");
   const bool spp = !strcmp(kind, "spp"), tpp = !strcmp(kind, "tpp");  // bf16 patch-staged (conv_patch.hip)
   const bool sp = wino || spp || !strcmp(kind, "sp"), tp = winot || tpp || !strcmp(kind, "tp");
   ConvParams p;
@@ -113,10 +115,10 @@ int main(int argc, char** argv) {
   p.relu = 1;
   const size_t nx = (size_t)N * T * H * W * Cin, ny = (size_t)p.M * Cout;
   p.x = bf ? to_bf16_dev(nx, 0.f, 1.f, 1) : dev_random(nx, 0.f, 1.f, 1);
-  const size_t nw = wino4 ? (size_t)(Cout / 48) * (Cin / 8) * 14336 : winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
+  const size_t nw = wino4w ? wino4w_weight_floats(Cin, Cout) : wino4 ? (size_t)(Cout / 48) * (Cin / 8) * 14336 : winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
   p.w = bf ? to_bf16_dev(nw, -0.05f, 0.05f, 2) : dev_random(nw, -0.05f, 0.05f, 2);
   p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
-  p.res = (getenv("CB_NORES") || wino4) ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
+  p.res = (getenv("CB_NORES") || wino4 || wino4w) ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
   CK(hipMalloc(&p.y, ny * 4));
   // ko 710..719 (fp32 direct convs): conv_dma_x3 on the split-bf16 image of the same weights,
   // split-K into ko - 710 K ranges when >= 2
@@ -144,7 +146,8 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   auto launch = [&](int ko) {
-    if (wino4) CK(ko ? launch_wino4_ko(p, s, ko) : launch_wino4(p, s));
+    if (wino4w) CK(ko ? launch_wino4w_ko(p, s, ko) : launch_wino4w(p, s));
+    else if (wino4) CK(ko ? launch_wino4_ko(p, s, ko) : launch_wino4(p, s));
     else if (winor) CK(launch_winor_ko(p, s, ko));
     else if (winoqp) CK(launch_winoq_probe(p, s, ko));
     else if (winoq) CK(launch_winoq_ko(p, s, ko));
