@@ -8,7 +8,7 @@
 // which DMAs the same raw patch and transforms it again (FETCH 4.3x the input bytes, transform and DMA
 // knock-outs 0.25 + 0.27 ms of a 2.1-ms launch, profiles/r03f_wino4_knockouts.txt). Here one block
 // covers 16 NTN output channels (NTN = 9: all 144 of layer1, half of layer2's 288, a quarter of layer3's
-// 576; NTN = 6 / 5 for 480 / 240): the patch is DMA'd and transformed once per tile group and every
+// 576; NTN = 6 for 480): the patch is DMA'd and transformed once per tile group and every
 // transformed value feeds NTN MFMAs instead of 3. The accumulators (9 Winograd elements x NTN x 4 =
 // 324 registers at NTN = 9) need one wave per SIMD: 4-wave blocks, one per CU, 512 registers per lane.
 // With no partner wave on the SIMD, U streams through a register ring UQ f32x4 loads deep (≈1800 MFMA
@@ -30,7 +30,7 @@ namespace {
 template <int NTN>
 struct W4W {
   static constexpr int NV = 18 * NTN;
-  static constexpr int UQ = NTN == 9 ? 14 : NTN == 6 ? 9 : 12;
+  static constexpr int UQ = NTN == 9 ? 14 : 9;
   static constexpr int NU = (NV + 4 * UQ - 1) / (4 * UQ) * UQ;
 };
 
@@ -61,7 +61,8 @@ constexpr int w4w_lds() {
 
 // C8: 8-channel-blocked output. DPW: DMA instructions per wave per chunk (W4Ring). KO: timing
 // knock-outs for tools/convbench (0 in the product; results are wrong otherwise): 1 no transform,
-// 2 no U loads in the loop, 4 no epilogue, 8 no DMAs in the loop.
+// 2 no U loads in the loop, 4 no epilogue, 8 no DMAs in the loop, 128 the epilogue without its output
+// stores.
 template <int NTN, bool C8, int DPW, int KO = 0>
 __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv_wino4w(ConvParams p,
                                                                                                       W4Geo g) {
@@ -325,16 +326,22 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
         }
         const size_t pix = (size_t)(uf * H + 4 * uty + aa) * W + uxx;
         const size_t off = C8 ? (size_t)(co >> 3) * plane + pix * 8 + (co & 7) : pix * CO + co;
-        *reinterpret_cast<f32x4*>(yout + off) = o;
+        if constexpr ((KO & 128) != 0) {  // probe: no output stores
+          if (o[0] == 1234.5f) *reinterpret_cast<f32x4*>(yout + off) = o;
+        } else {
+          *reinterpret_cast<f32x4*>(yout + off) = o;
+        }
       }
     }
   }
 }
 
-// NTN for a Cout: the widest of 9, 6, 5 N tiles dividing it (0: none)
+// NTN for a Cout: the widest of 9, 6 N tiles dividing it (0: none). NTN = 5 (layer2's 240 channels)
+// compiles but ran 0.785 vs conv_wino4's 0.754 ms (r04b): the 80-channel block pays the one-wave-per-SIMD
+// serialisation without enough reuse to win it back, so conv_wino4 keeps that conv.
 int wino4w_ntn(int cout) {
   if (cout % 16) return 0;
-  for (int n : {9, 6, 5})
+  for (int n : {9, 6})
     if ((cout / 16) % n == 0) return n;
   return 0;
 }
@@ -376,11 +383,7 @@ hipError_t launch_wino4w(const ConvParams& p, hipStream_t s) {
   int nb;
   const int ntn = wino4w_ntn(p.Cout);
   wino4_geometry(p, &g, &nb, 16 * ntn);
-  switch (ntn) {
-    case 9: return launch_w4w_dpw<9>(p, g, nb, s);
-    case 6: return launch_w4w_dpw<6>(p, g, nb, s);
-    default: return launch_w4w_dpw<5>(p, g, nb, s);
-  }
+  return ntn == 9 ? launch_w4w_dpw<9>(p, g, nb, s) : launch_w4w_dpw<6>(p, g, nb, s);
 }
 
 // Every block issues 16 MFMA rows (tiles, the group's padding included) x 36 elements x Cin x 16 NTN.
@@ -395,7 +398,7 @@ double wino4w_exec_gflop(const ConvParams& p) {
 size_t wino4w_weight_floats(int cin_p, int cout_p) {
   const int ntn = wino4w_ntn(cout_p);
   if (!ntn) return 0;
-  const int nu = ntn == 9 ? W4W<9>::NU : ntn == 6 ? W4W<6>::NU : W4W<5>::NU;
+  const int nu = ntn == 9 ? W4W<9>::NU : W4W<6>::NU;
   return (size_t)(cout_p / (16 * ntn)) * (cin_p / 8) * W4_WAVES * nu * 256;
 }
 
@@ -411,7 +414,7 @@ void wino4w_transform_weights(const double* w, int cout, int cin, int cout_p, in
                                  {1.0 / 24, -1.0 / 12, 1.0 / 6},
                                  {0, 0, 1}};
   const int ntn = wino4w_ntn(cout_p);
-  const int nu = ntn == 9 ? W4W<9>::NU : ntn == 6 ? W4W<6>::NU : W4W<5>::NU;
+  const int nu = ntn == 9 ? W4W<9>::NU : W4W<6>::NU;
   const int nch = cin_p / 8, cw = 16 * ntn;
   const size_t total = wino4w_weight_floats(cin_p, cout_p);
   for (size_t i = 0; i < total; ++i) U[i] = 0.f;
@@ -446,6 +449,7 @@ hipError_t launch_wino4w_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 4: return launch_w4w_dpw<9, 4>(p, g, nb, s);
     case 8: return launch_w4w_dpw<9, 8>(p, g, nb, s);
     case 15: return launch_w4w_dpw<9, 15>(p, g, nb, s);
+    case 128: return launch_w4w_dpw<9, 128>(p, g, nb, s);
     default: return launch_w4w_dpw<9>(p, g, nb, s);
   }
 }

@@ -597,9 +597,9 @@ def test_wino4_matches_wino2(model, shape):
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (3, 3, 24, 32, 32), (2, 3, 16, 64, 48),
                                    (1, 3, 16, 112, 224)])
 def test_wino4w_bitexact_vs_wino4(model, shape):
-    """conv_wino4w (wide output-channel blocks: 144 / 288 / 576 channels as 144-channel blocks, 240 as
-    80, 480 as 96) issues conv_wino4's products in conv_wino4's order (variant no_wino4w): the forward
-    is bit-identical, with the wide kernel really running."""
+    """conv_wino4w (wide output-channel blocks: 144 / 288 / 576 channels as 144-channel blocks, 480 as
+    96; 240 stays on conv_wino4) issues conv_wino4's products in conv_wino4's order (variant
+    no_wino4w): the forward is bit-identical, with the wide kernel really running."""
     rng = np.random.default_rng(47)
     x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
     model.engine.set_kernel_timing(True)
