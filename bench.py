@@ -63,6 +63,9 @@ def parse(argv=None):
     ap.add_argument("--fuse-method", default="simple")
     ap.add_argument("--batch-size", type=int, default=32, help="clips per forward call")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
+    ap.add_argument("--parity-random", type=int, default=1,
+                    help="also check the same workload with the random weight recipe against its CPU fixture "
+                         "(one untimed step; reported as 'parity_random_weights')")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal, several ranks on one GPU)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"], help="encoder compute dtype of the headline run")
     ap.add_argument("--extra-bf16", type=int, default=1,
@@ -449,7 +452,7 @@ def run_c1(args, model, world, rank, dev):
     fwd = forward_stats(ktimes, (hi - lo) * args.steps, GFLOP_PER_CLIP, peak)
     lv_frac = float(np.mean([o.float().mean().item() for o in out.values()])) if out else 0.0
     parity = northstar_parity(args, out[0], args.dtype) if 0 in out else None
-    parity_random = random_recipe_parity(args, model, step, args.dtype) if world == 1 else None
+    parity_random = random_recipe_parity(args, model, step, args.dtype) if world == 1 and args.parity_random else None
 
     bf16 = None
     if args.extra_bf16 and args.dtype == "fp32":

@@ -11,7 +11,7 @@ timeout -k 10 400 python -u bench.py > $out/bench.log 2>&1 || { echo "bench fail
 tail -1 $out/bench.log | cut -c1-400
 timeout -k 10 400 python -u bench.py --workload c2 --steps 5 --warmup 2 > $out/bench_c2.log 2>&1 || { echo "bench c2 failed"; tail -30 $out/bench_c2.log; exit 1; }
 tail -1 $out/bench_c2.log | cut -c1-300
-B="bench.py --steps 2 --warmup 1 --cpu-baseline 0 --extra-bf16 0 --extra-c3 0 --extra-stream 0"
+B="bench.py --steps 2 --warmup 1 --cpu-baseline 0 --extra-bf16 0 --extra-c3 0 --extra-stream 0 --parity-random 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f rocpd csv -T -d $out/trace -o t -- python3 $B > $out/trace.log 2>&1 || { echo "trace failed"; tail -30 $out/trace.log; exit 1; }
 find $out/trace -name 't_kernel_stats.csv' -exec cp {} $out/kernel_stats.csv \;
 if [ "$2" = quick ]; then
