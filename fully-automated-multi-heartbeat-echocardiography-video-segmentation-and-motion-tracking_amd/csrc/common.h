@@ -135,6 +135,8 @@ void winot_transform_weights(const double* w, int cout, int cin, int cout_p, int
 // Patch-staged bf16 implicit GEMM for stride-1 1x3x3 and 3x1x1 convs (conv_patch.hip); p.w = conv_dma's
 // image.
 bool patch_bf16_supported(const ConvParams& p);
+bool patch32_bf16_supported(const ConvParams& p);
+hipError_t launch_patch32_bf16(const ConvParams& p, hipStream_t s);
 hipError_t launch_patch_bf16(const ConvParams& p, hipStream_t s);
 // bf16 stem (config[4]): fp32 4-channel clip split into bf16 hi + lo in registers; p.w = hi and lo
 // images, each [64][7][8][4] bf16.

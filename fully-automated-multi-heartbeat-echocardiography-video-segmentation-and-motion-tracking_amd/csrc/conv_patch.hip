@@ -34,6 +34,7 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
@@ -83,7 +84,9 @@ __device__ inline void for_taps(std::integer_sequence<int, I...>, F&& f) {
 
 // S = B ring depth (B(s) is fetched S-1 steps ahead); OCC = blocks per CU (the LDS budget and the
 // register cap follow from it).
-template <int NT, int KT, int FR, int S, int OCC>
+// STG: LDS-staged output stores (the product form; false = 8-B stores from the accumulator layout,
+// convbench A/B)
+template <int NT, int KT, int FR, int S, int OCC, bool STG = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void conv_patch_bf16(
     ConvParams p, int n_tiles, int ptw, int npt, int t_tiles) {
   using G = PGeo<KT, FR>;
@@ -234,35 +237,76 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   // epilogue: acc[i][j] holds channels n0 + 16j + 4q .. +3 of block voxel 16*(MT*wid + i) + l16
   const __bf16* res = reinterpret_cast<const __bf16*>(p.res);
   __bf16* y = reinterpret_cast<__bf16*>(p.y);
-#pragma unroll
-  for (int i = 0; i < MT; ++i) {
-    const int m = 16 * (MT * wid + i) + l16, f = m >> 6, px = m & 63;
-    const int to = t0 + f;
-    size_t gm;
+  // global voxel index of block voxel m (false outside the map)
+  auto voxel = [&](int m, size_t& gm) __attribute__((always_inline)) {
+    const int f = m >> 6, px = m & 63, to = t0 + f;
     if constexpr (G::SPATIAL) {
       const int ho = h0 + (px >> 3), wo = w0 + (px & 7);
-      if (!(to < p.To && ho < p.Ho && wo < p.Wo)) continue;
-      gm = (((size_t)clip * p.To + to) * p.Ho + ho) * p.Wo + wo;
+      gm = (((size_t)clip * p.To + to) * p.Ho + (ho < p.Ho ? ho : 0)) * p.Wo + (wo < p.Wo ? wo : 0);
+      return to < p.To && ho < p.Ho && wo < p.Wo;
     } else {
       const int hw = hw0 + px;
-      if (!(to < p.To && hw < HW)) continue;
-      gm = ((size_t)clip * p.To + to) * HW + hw;
+      gm = ((size_t)clip * p.To + to) * HW + (hw < HW ? hw : 0);
+      return to < p.To && hw < HW;
     }
+  };
+  auto finish = [&](int i, int j, size_t gm) __attribute__((always_inline)) {
+    const int n = n0 + j * 16 + 4 * q;
+    f32x4 v = acc[i][j];
+    if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
+    if (res) {
+      const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + gm * p.Cout + n);
+      v += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
+    }
+    if (p.relu) {
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int n = n0 + j * 16 + 4 * q;
-      const size_t o = gm * p.Cout + n;
-      f32x4 v = acc[i][j];
-      if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
-      if (res) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + o);
-        v += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
-      }
-      if (p.relu) {
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    return bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  };
+  if constexpr (!STG) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    for (int i = 0; i < MT; ++i) {
+      size_t gm;
+      if (!voxel(16 * (MT * wid + i) + l16, gm)) continue;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) *reinterpret_cast<bf16x4*>(y + gm * p.Cout + n0 + j * 16 + 4 * q) = finish(i, j, gm);
+    }
+  } else {
+    // LDS-staged: a lane's 8-B pieces hit 16 voxels per store instruction (16 partial lines); staged
+    // in the dead patch / weight buffers as [16 MT voxels][NT*32 B + 16] per wave, they leave as
+    // MT*NT/2 16-B-per-lane stores of whole voxel segments (contiguous runs when the block covers
+    // every channel). convbench: see profiles/r04_patch32_bf16.txt
+    // MH m tiles per pass: all MT when the 4 waves' staging fits the block's LDS, else half
+    constexpr int SEG = NT * 32, VS = SEG + 16;
+    constexpr int MH = 4 * 16 * MT * VS <= LDS ? MT : MT / 2, INS = 16 * MH * SEG / 1024;
+    static_assert(4 * 16 * MH * VS <= LDS, "staging fits the block's LDS");
+    static_assert(16 * MH * SEG % 1024 == 0, "whole store instructions");
+    char* st = smem + wid * 16 * MH * VS;
+    __builtin_amdgcn_s_barrier();  // every wave is past its last patch / weight read
+#pragma unroll
+    for (int i0 = 0; i0 < MT; i0 += MH) {
+#pragma unroll
+      for (int i = i0; i < i0 + MH; ++i) {
+        size_t gm;
+        voxel(16 * (MT * wid + i) + l16, gm);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          *reinterpret_cast<bf16x4*>(st + (16 * (i - i0) + l16) * VS + (16 * j + 4 * q) * 2) = finish(i, j, gm);
       }
-      *reinterpret_cast<bf16x4*>(y + o) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int k = 0; k < INS; ++k) {
+        const int e = 1024 * k + 16 * lane, v = e / SEG, off = e - v * SEG;
+        const bf16x8 val = *reinterpret_cast<const bf16x8*>(st + v * VS + off);
+        size_t gm;
+        if (voxel(16 * (MT * wid + i0) + v, gm)) *reinterpret_cast<bf16x8*>(y + gm * p.Cout + n0 + off / 2) = val;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
 }
@@ -292,11 +336,11 @@ PatchGrid patch_grid(const ConvParams& p, int fr) {
   return g;
 }
 
-template <int NT, int KT, int FR, int S = 3>
+template <int NT, int KT, int FR, int S = 3, bool STG = true>
 hipError_t launch_p(const ConvParams& p, hipStream_t s) {
   const PatchGrid g = patch_grid(p, FR);
   const int n_tiles = p.Cout / (16 * NT);
-  hipLaunchKernelGGL((conv_patch_bf16<NT, KT, FR, S, patch_occ<NT, KT, FR, S>()>), dim3((unsigned)(g.base * n_tiles)),
+  hipLaunchKernelGGL((conv_patch_bf16<NT, KT, FR, S, patch_occ<NT, KT, FR, S>(), STG>), dim3((unsigned)(g.base * n_tiles)),
                      dim3(256), 0, s, p, n_tiles, g.ptw, g.npt, g.tt);
   return hipGetLastError();
 }
@@ -361,7 +405,350 @@ int patch_pick_nt(const ConvParams& p, int force_nt) {
   return pick;
 }
 
+// ---------------------------------------------------------------------------------------------
+// conv_patch32_bf16: the spatial 1x3x3 form on v_mfma_f32_32x32x16_bf16 (round 4).
+//
+// conv_patch_bf16's 16x16x32 tiles read 12 LDS fragments per 20 MFMAs of 16 cycles; a 32x32x16 MFMA
+// takes the same cycles per FLOP and each 16-B fragment feeds twice the products, so here a wave
+// owns one whole 8x8-pixel output frame (64 voxels = two 32-voxel column blocks) x 32*NB channels:
+// per 32-deep K step 2*NB weight + 4 patch fragments for 4*NB MFMAs of 32 cycles (14 per 640 cycles
+// at NB = 5 instead of 12 per 320). Block = 4 frames (one per wave) x 8x8 pixels, 256 voxels, so
+// each weight byte DMA'd to LDS serves twice the voxels of the 2-frame kernel.
+//  * D^T = W . X^T: A operand = 32 weight rows (output channels) x 16 k, B operand = 16 k x 32
+//    voxels; lane l (r = l & 31, h = l >> 5) reads row / voxel r, k = 8h .. 8h+7 of the K half;
+//  * patch reads are bank-conflict-free: ds_read_b128 serves a wave in the lane groups
+//    {0-3,12-15,20-27}, {4-11,16-19,28-31} (and the same +32); lane r of a column block reads
+//    voxel vmap(r), which puts each lane group on two whole 8-pixel rows of the frame tile, and the
+//    16-B slot q of patch pixel (row, col) is stored at q ^ ((col >> 2 & 1) | (row & 1) << 1):
+//    the 4 pixels of a group that share a bank quad (pixel index mod 4, 10-pixel rows) are two
+//    columns 4 apart in each of two adjacent rows, so the swizzle separates all four at every tap;
+//  * weight rows keep conv_patch_bf16's swizzle (slot q of row n at q ^ g[(n >> 2) & 3]), which is
+//    also conflict-free for the 32-row operand's lane groups;
+//  * the second 16-deep half of a 32-channel K step is the same address ^ 32 (slot bit 1);
+//  * the accumulator of column block cb holds, in register i, channel 32rb + 8(i >> 2) + 4h + (i & 3)
+//    of voxel vmap(r): 4 consecutive channels per lane, 8-B bf16 stores as before.
+// The weight ring has S = 2 stages (LDS 2 x 25 KiB patch + 2 x NB x 2 KiB: two blocks per CU).
+
+__device__ inline int p32_vmap(int r) {  // lane row r of a 32-voxel column block -> voxel 0..31
+  return r < 4 ? r : r < 12 ? r + 12 : r < 16 ? r - 8 : r < 20 ? r + 8 : r < 28 ? r - 12 : r;
+}
+__device__ inline int p32_swz(int row, int col) { return ((col >> 2) & 1) | ((row & 1) << 1); }
+
+// MODE bit 0: LDS-staged epilogue (the product form); bits 1..5 are convbench knock-outs (timing only):
+// 2 no weight DMAs in the loop, 4 no patch DMAs in the loop, 8 no step barriers, 16 no MFMAs,
+// 32 no output stores, 64 non-temporal output stores
+template <int NB, int S, int OCC, int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void conv_patch32_bf16(
+    ConvParams p, int n_tiles, int ptw, int npt, int t_tiles) {
+  constexpr int FR = 4, TAPS = 9, PC = 10, FPIX = 100;
+  constexpr int PIECES = (FR * FPIX + 15) / 16, PBYTES = PIECES * 1024;
+  constexpr int WP = 2 * NB;                                   // weight pieces (16 rows x 64 B) per step
+  constexpr int PW = (PIECES + 3) / 4, BW = (WP + 3) / 4;      // DMAs per wave (uniform counts)
+  constexpr int B_STAGE = WP * 1024, B0 = 2 * PBYTES, SINK = B0 + S * B_STAGE;
+  constexpr int LDS = SINK + 1024;
+  static_assert(OCC * LDS <= 160 * 1024, "LDS budget");
+  static_assert(S >= 2 && S <= TAPS + 1, "wait counts below assume S - 1 <= TAPS");
+  __shared__ __align__(16) char smem[LDS];
+
+  const __bf16* x = reinterpret_cast<const __bf16*>(p.x);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, h = lane >> 5;
+  int tile = xcd_swizzle_p(blockIdx.x, gridDim.x);
+  const int n0 = (tile % n_tiles) * 32 * NB;
+  tile /= n_tiles;
+  const int pt = tile % npt;
+  tile /= npt;
+  const int t0 = (tile % t_tiles) * FR;
+  const int clip = tile / t_tiles;
+  const int h0 = (pt / ptw) * 8, w0 = (pt % ptw) * 8;
+  const int Cin = p.Cin;
+
+  // patch DMA: piece j = wid + 4*i writes pixels 16j .. 16j+15, lane -> pixel 16j + lane/4, physical
+  // slot lane & 3 (fetches logical slot (lane & 3) ^ swz); pixels outside the map read the zero block
+  int pv[PW];
+  unsigned psl[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int pix = (wid + 4 * i) * 16 + (lane >> 2);
+    const int f = pix / FPIX, rr = pix - f * FPIX, pr = rr / PC, pc = rr - pr * PC;
+    psl[i] = (unsigned)(((lane & 3) ^ p32_swz(pr, pc)) * 16);
+    pv[i] = -1;
+    if (pix < FR * FPIX) {
+      const int ti = t0 + f, hi = h0 - 1 + pr, wi = w0 - 1 + pc;
+      if (ti < p.Ti && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi)
+        pv[i] = ((clip * p.Ti + ti) * p.Hi + hi) * p.Wi + wi;
+    }
+  }
+  auto issue_patch = [&](int c, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int j = wid + 4 * i;
+      const void* src = pv[i] >= 0 ? (const void*)(reinterpret_cast<const char*>(x + (size_t)pv[i] * Cin + 32 * c) + psl[i])
+                                   : p.zero;
+      dma16(src, smem + (j < PIECES ? buf * PBYTES + j * 1024 : SINK));
+    }
+  };
+  const char* wb = reinterpret_cast<const char*>(p.w) + (size_t)n0 * p.Kp * 2;
+  unsigned boff[BW];
+  {
+    const int drow = lane >> 2, dq = (lane & 3) ^ gsw((drow >> 2) & 3);
+#pragma unroll
+    for (int i = 0; i < BW; ++i) {
+      const int j = wid + 4 * i;
+      boff[i] = (unsigned)(((j < WP ? j : 0) * 16 + drow) * p.Kp + 8 * dq) * 2u;
+    }
+  }
+  const int nc = Cin / 32;
+  auto issue_b = [&](int c, int tap, int slot) __attribute__((always_inline)) {
+    const char* base = wb + (size_t)(tap * Cin + 32 * (c < nc ? c : 0)) * 2;
+#pragma unroll
+    for (int i = 0; i < BW; ++i) {
+      const int j = wid + 4 * i;
+      dma16(base, boff[i], smem + (j < WP ? B0 + slot * B_STAGE + j * 1024 : SINK));
+    }
+  };
+
+  f32x16 acc[NB][2];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  // patch fragment addresses (K half 0; half 1 is ^ 32) of this lane's voxel in column block cb at
+  // every tap, patch buffer 0
+  const int vox = p32_vmap(r32);
+  int paddr[TAPS][2];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int row = 4 * cb + (vox >> 3), col = vox & 7;
+#pragma unroll
+    for (int tap = 0; tap < TAPS; ++tap) {
+      const int pr = row + tap / 3, pc = col + tap % 3;
+      const int pix = wid * FPIX + pr * PC + pc;
+      paddr[tap][cb] = pix * 64 + ((h ^ p32_swz(pr, pc)) << 4);
+    }
+  }
+  const int w_rd0 = B0 + r32 * 64 + ((h ^ gsw((r32 >> 2) & 3)) << 4), w_rd1 = w_rd0 ^ 32;
+
+  issue_patch(0, 0);
+#pragma unroll
+  for (int k = 0; k < S - 1; ++k) issue_b(k / TAPS, k % TAPS, k);
+  int slot = 0;
+
+  for (int c = 0; c < nc; ++c) {
+    const bool more = c + 1 < nc;
+    const int pbuf = (c & 1) * PBYTES;
+    for_taps(std::make_integer_sequence<int, TAPS>{}, [&](auto tc) __attribute__((always_inline)) {
+      constexpr int TAP = decltype(tc)::value;
+      if constexpr (MODE & 6) {
+        vm_wait<0>();
+      } else if constexpr (TAP >= 1 && TAP <= S - 1) {
+        if (more) vm_wait<(S - 2) * BW + PW>();
+        else vm_wait<(S - 2) * BW>();
+      } else {
+        vm_wait<(S - 2) * BW>();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(MODE & 8)) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int T2 = (TAP + S - 1) % TAPS, C2 = (TAP + S - 1) / TAPS;
+      const int slot_new = slot == 0 ? S - 1 : slot - 1;
+      if constexpr (!(MODE & 2)) issue_b(c + C2, T2, slot_new);
+      if constexpr (TAP == 0 && !(MODE & 4)) {
+        if (more) issue_patch(c + 1, (c + 1) & 1);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const char* bs = smem + (kk ? w_rd1 : w_rd0) + slot * B_STAGE;
+        bf16x8 a[2], b[NB];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          a[cb] = *reinterpret_cast<const bf16x8*>(smem + pbuf + (paddr[TAP][cb] ^ (32 * kk)));
+#pragma unroll
+        for (int rb = 0; rb < NB; ++rb) b[rb] = *reinterpret_cast<const bf16x8*>(bs + rb * 2048);
+#pragma unroll
+        for (int rb = 0; rb < NB; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            if constexpr (MODE & 16) {
+              acc[rb][cb][0] += (float)b[rb][0] * (float)a[cb][kk];
+            } else {
+              acc[rb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[rb], a[cb], acc[rb][cb], 0, 0, 0);
+            }
+          }
+      }
+      slot = slot + 1 == S ? 0 : slot + 1;
+    });
+  }
+  vm_wait<0>();
+
+  // epilogue: acc[rb][cb][i] = channel n0 + 32rb + 8(i >> 2) + 4h + (i & 3) of voxel vox of column
+  // block cb (frame t0 + wid, frame-tile row 4cb + vox / 8, column vox % 8)
+  const __bf16* res = reinterpret_cast<const __bf16*>(p.res);
+  __bf16* y = reinterpret_cast<__bf16*>(p.y);
+  const int to = t0 + wid;
+  auto finish = [&](int rb, int cb, int g, size_t gm) __attribute__((always_inline)) {
+    const int n = n0 + 32 * rb + 8 * g + 4 * h;
+    f32x4 v = {acc[rb][cb][4 * g], acc[rb][cb][4 * g + 1], acc[rb][cb][4 * g + 2], acc[rb][cb][4 * g + 3]};
+    if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
+    if (res) {
+      const bf16x4 rv = *reinterpret_cast<const bf16x4*>(res + gm * p.Cout + n);
+      v += f32x4{(float)rv[0], (float)rv[1], (float)rv[2], (float)rv[3]};
+    }
+    if (p.relu) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    return bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  };
+  if constexpr (MODE & 32) {  // knock-out: no stores (every accumulator kept live)
+    float sum = 0.f;
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sum += acc[rb][cb][e];
+    if (sum == 12345.f) y[lane] = (__bf16)sum;
+  } else if constexpr ((MODE & 1) == 0) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int ho = h0 + 4 * cb + (vox >> 3), wo = w0 + (vox & 7);
+      if (!(to < p.To && ho < p.Ho && wo < p.Wo)) continue;
+      const size_t gm = (((size_t)clip * p.To + to) * p.Ho + ho) * p.Wo + wo;
+#pragma unroll
+      for (int rb = 0; rb < NB; ++rb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) *reinterpret_cast<bf16x4*>(y + gm * p.Cout + n0 + 32 * rb + 8 * g + 4 * h) = finish(rb, cb, g, gm);
+    }
+  } else {
+    // LDS-staged stores: a lane's 8-B pieces are scattered over 32 voxels (32 partial lines per store
+    // instruction); staged through the dead patch buffers as [32 voxels][NB*64 B + 16], each column
+    // block leaves as NB*2 16-B-per-lane stores of whole voxel segments (contiguous 8-pixel rows
+    // when the block covers every channel)
+    constexpr int SEG = NB * 64, VS = SEG + 16, INS = SEG * 32 / 1024;
+    static_assert(4 * 32 * VS <= 2 * PBYTES, "staging fits the patch buffers");
+    char* st = smem + wid * 32 * VS;
+    __builtin_amdgcn_s_barrier();  // every wave is past its last patch / weight read
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int ho_l = h0 + 4 * cb + (vox >> 3), wo_l = w0 + (vox & 7);
+      const size_t gm_l = (((size_t)clip * p.To + to) * p.Ho + (ho_l < p.Ho ? ho_l : 0)) * p.Wo + (wo_l < p.Wo ? wo_l : 0);
+#pragma unroll
+      for (int rb = 0; rb < NB; ++rb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<bf16x4*>(st + vox * VS + (32 * rb + 8 * g + 4 * h) * 2) = finish(rb, cb, g, gm_l);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int k = 0; k < INS; ++k) {
+        const int e = 1024 * k + 16 * lane, v = e / SEG, off = e - v * SEG;
+        const bf16x8 val = *reinterpret_cast<const bf16x8*>(st + v * VS + off);
+        const int ho = h0 + 4 * cb + (v >> 3), wo = w0 + (v & 7);
+        if (to < p.To && ho < p.Ho && wo < p.Wo) {
+          const size_t gm = (((size_t)clip * p.To + to) * p.Ho + ho) * p.Wo + wo;
+          if constexpr (MODE & 64) {
+            __builtin_nontemporal_store(val, reinterpret_cast<bf16x8*>(y + gm * p.Cout + n0 + off / 2));
+          } else {
+            *reinterpret_cast<bf16x8*>(y + gm * p.Cout + n0 + off / 2) = val;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+}
+
+template <int NB, int S = 2>
+constexpr int patch32_occ() {
+  constexpr int lds = 2 * 25 * 1024 + S * NB * 2048 + 1024;
+  constexpr int occ = 160 * 1024 / lds;
+  return occ > 4 ? 4 : occ;
+}
+
+template <int NB, int S = 2, int EPI = 1>
+hipError_t launch_p32(const ConvParams& p, hipStream_t s) {
+  const PatchGrid g = patch_grid(p, 4);
+  const int n_tiles = p.Cout / (32 * NB);
+  hipLaunchKernelGGL((conv_patch32_bf16<NB, S, patch32_occ<NB, S>(), EPI>), dim3((unsigned)(g.base * n_tiles)), dim3(256), 0,
+                     s, p, n_tiles, g.ptw, g.npt, g.tt);
+  return hipGetLastError();
+}
+
+// N tile (32-channel blocks). Product rule: NB = 5 (160-channel blocks: the bf16 layer1 spatial
+// convs, 64 -> 160) on grids of >= 512 blocks; everywhere else conv_patch_bf16 is as fast or faster
+// (convbench, profiles/r04_patch32_bf16.txt: layer1 0.686 vs 0.726 ms, layer2 288 channels at NB 3
+// 0.325 vs 0.313, layer3 576 at NB 3 0.152 vs 0.156, layer4 1152 at NB 2 0.114 vs 0.088). 0: not
+// taken. force_nb > 0 (convbench, CLASFV_PATCH_NT = -NB) takes any NB that divides.
+int patch32_pick_nb(const ConvParams& p, int force_nb) {
+  if (p.Cout % 32) return 0;
+  const int n32 = p.Cout / 32;
+  if (force_nb > 0) return (force_nb <= 5 && force_nb >= 2 && n32 % force_nb == 0) ? force_nb : 0;
+  return n32 % 5 == 0 && patch_grid(p, 4).base * (n32 / 5) >= 512 ? 5 : 0;
+}
+
 }  // namespace
+
+bool patch32_bf16_supported(const ConvParams& p) {
+  if (!p.in_bf16 || !p.out_bf16 || p.stem || p.x2) return false;
+  if (p.st != 1 || p.sh != 1 || p.sw != 1) return false;
+  if (!(p.KT == 1 && p.KH == 3 && p.KW == 3 && p.pt == 0 && p.ph == 1 && p.pw == 1)) return false;
+  if (p.Cin % 32 || p.Kp != 9 * p.Cin) return false;
+  if (p.To != p.Ti || p.Ho != p.Hi || p.Wo != p.Wi) return false;
+  if (patch32_pick_nb(p, p.patch_nt < 0 ? -p.patch_nt : 0) == 0) return false;
+  if ((long)p.N * p.Ti * p.Hi * p.Wi >= (1L << 31) / 2) return false;
+  return true;
+}
+
+hipError_t launch_patch32_bf16(const ConvParams& p, hipStream_t s) {
+  if (!patch32_bf16_supported(p)) return hipErrorInvalidValue;
+  switch (patch32_pick_nb(p, p.patch_nt < 0 ? -p.patch_nt : 0)) {  // CLASFV_PATCH_NT < 0: force NB
+    case 5: return launch_p32<5>(p, s);
+    case 4: return launch_p32<4>(p, s);
+    case 3: return launch_p32<3>(p, s);
+    case 2: return launch_p32<2>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+#ifdef CLASFV_KNOCKOUTS
+// tools/convbench.hip: epi = MODE (0 = direct 8-B stores from the accumulator layout, 1 = LDS-staged,
+// odd values above 1: knock-outs at NB 5)
+hipError_t launch_patch32_bf16_epi(const ConvParams& p, hipStream_t s, int epi) {
+  if (!patch32_bf16_supported(p)) return hipErrorInvalidValue;
+  const int nb = patch32_pick_nb(p, p.patch_nt < 0 ? -p.patch_nt : 0);
+  if (epi == 1) return launch_patch32_bf16(p, s);
+  if (epi == 0) {
+    switch (nb) {
+      case 5: return launch_p32<5, 2, 0>(p, s);
+      case 4: return launch_p32<4, 2, 0>(p, s);
+      case 3: return launch_p32<3, 2, 0>(p, s);
+      case 2: return launch_p32<2, 2, 0>(p, s);
+    }
+  }
+  if (nb != 5) return hipErrorInvalidValue;
+  switch (epi) {  // knock-outs (MODE bits), NB 5
+    case 3: return launch_p32<5, 2, 3>(p, s);
+    case 5: return launch_p32<5, 2, 5>(p, s);
+    case 7: return launch_p32<5, 2, 7>(p, s);
+    case 9: return launch_p32<5, 2, 9>(p, s);
+    case 15: return launch_p32<5, 2, 15>(p, s);
+    case 17: return launch_p32<5, 2, 17>(p, s);
+    case 33: return launch_p32<5, 2, 33>(p, s);
+    case 47: return launch_p32<5, 2, 47>(p, s);
+    case 31: return launch_p32<5, 2, 31>(p, s);
+    case 65: return launch_p32<5, 2, 65>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+#endif
 
 bool patch_bf16_supported(const ConvParams& p) {
   if (!p.in_bf16 || !p.out_bf16 || p.stem || p.x2) return false;
@@ -413,10 +800,30 @@ hipError_t ko_s(const ConvParams& p, int st, int nt, hipStream_t s) {
   }
   return hipErrorInvalidValue;
 }
+// the product configuration with the direct (unstaged) epilogue
+template <int KT>
+hipError_t direct_nt(const ConvParams& p, int nt, hipStream_t s) {
+  constexpr int FR = product_fr<KT>(), S = product_s<KT>();
+  switch (nt) {
+    case 10: return launch_p<10, KT, FR, S, false>(p, s);
+    case 9: return launch_p<9, KT, FR, S, false>(p, s);
+    case 8: return launch_p<8, KT, FR, S, false>(p, s);
+    case 6: return launch_p<6, KT, FR, S, false>(p, s);
+    case 5: return launch_p<5, KT, FR, S, false>(p, s);
+    case 4: return launch_p<4, KT, FR, S, false>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
 }  // namespace
 
+// ko 10000: the product configuration with direct 8-B output stores (no LDS staging)
 hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko) {
   if (ko == 0) return launch_patch_bf16(p, s);
+  if (ko == 10000) {
+    if (!patch_bf16_supported(p)) return hipErrorInvalidValue;
+    const int nt = patch_pick_nt(p, p.patch_nt);
+    return p.KT == 1 ? direct_nt<1>(p, nt, s) : direct_nt<3>(p, nt, s);
+  }
   const int fr = ko / 1000, st = ko / 100 % 10, nt = ko % 100;
   if (p.Cout % (16 * nt)) return hipErrorInvalidValue;
   if (fr == 2) return p.KT == 1 ? ko_s<1, 2>(p, st, nt, s) : ko_s<3, 2>(p, st, nt, s);

@@ -613,6 +613,29 @@ def test_wino4w_bitexact_vs_wino4(model, shape):
     assert torch.equal(s_w, s_4) and torch.equal(m_w, m_4)
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 32, 112, 112), (3, 3, 24, 80, 112)])
+def test_bf16_patch32_bitexact_vs_patch16(shape):
+    """config[4]: the bf16 layer1 spatial convs on conv_patch32_bf16 (v_mfma_f32_32x32x16_bf16, 4-frame
+    blocks, LDS-staged stores) against conv_patch_bf16 (16x16x32, 2-frame blocks; variant no_patch32):
+    the same bf16 products summed in fp32 -- bit-identical outputs on the box (convbench CB_CHECK over
+    4.8e8 layer1 outputs, profiles/r04_patch32_bf16.txt), asserted here on the whole forward (the
+    kernel takes grids of >= 512 blocks: 2 clips at 32x112x112; 3 clips with 40x56 layer1 maps)."""
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    rng = np.random.default_rng(53)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    m16 = R2plus1D_18_MotionNet(pretrained=False, dtype="bf16")
+    m16.engine.set_kernel_timing(True)
+    s_32, mo_32 = m16(x)
+    kt = m16.engine.kernel_timing()
+    m16.engine.set_kernel_timing(False)
+    assert "conv_patch32_bf16" in kt
+    m16.set_kernel_variants("no_patch32")
+    s_16, mo_16 = m16(x)
+    m16.set_kernel_variants()
+    assert torch.isfinite(s_32).all()
+    assert torch.equal(s_32, s_16) and torch.equal(mo_32, mo_16)
+
+
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 8, 32, 48)])
 def test_decoder_x3_matches_fp32_mfma(model, shape):
     """The fp32 engines' comb_2 on six split-bf16 products (hi/mid/lo pieces of both operands, fp32

@@ -25,6 +25,7 @@ hipError_t launch_dma_x3_cfg(const ConvParams& p, int mt, int nt, int S, hipStre
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
 hipError_t launch_patch_bf16_v1(const ConvParams& p, hipStream_t s);
 hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
+hipError_t launch_patch32_bf16_epi(const ConvParams& p, hipStream_t s, int epi);
 hipError_t launch_winoq_probe(const ConvParams& p, hipStream_t s, int ko);
 void winos_stamps(unsigned long long* out);
 
@@ -155,6 +156,13 @@ int main(int argc, char** argv) {
     else if (wino) CK(launch_wino_ko(p, s, ko));
     else if (winot) CK(launch_winot_ko(p, s, ko));
     else if ((spp || tpp) && ko == 901) CK(launch_patch_bf16_v1(p, s));
+    else if (spp && ko >= 950 && ko < 970) {  // conv_patch32_bf16 (32x32x16 tiles); 951..955: NB forced;
+      ConvParams q = p;                        // 960..965: direct-store epilogue
+      q.patch_nt = ko % 10 ? -(ko % 10) : 0;
+      CK(launch_patch32_bf16_epi(q, s, ko < 960));
+    } else if (spp && ko >= 970 && ko < 1040) {  // conv_patch32_bf16 knock-outs: MODE = ko - 970
+      CK(launch_patch32_bf16_epi(p, s, ko - 970));
+    }
     else if ((spp || tpp) && ko != 900) CK(launch_patch_bf16_ko(p, s, ko));
     else {
       int mt, bn;
@@ -209,15 +217,27 @@ int main(int argc, char** argv) {
   // CB_CHECK=1: every variant's output against the first one's (bitwise; max |diff| printed)
   if (getenv("CB_CHECK") && kos.size() > 1) {
     std::vector<float> ref(ny), got(ny);
+    auto fetch = [&](std::vector<float>& out) {  // bf16 outputs widened to float
+      if (!bf) {
+        CK(hipMemcpy(out.data(), p.y, ny * 4, hipMemcpyDeviceToHost));
+        return;
+      }
+      std::vector<uint16_t> h(ny);
+      CK(hipMemcpy(h.data(), p.y, ny * 2, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < ny; ++i) {
+        const uint32_t u = (uint32_t)h[i] << 16;
+        memcpy(&out[i], &u, 4);
+      }
+    };
     CK(hipMemset(p.y, 0, ny * 4));
     launch(kos[0]);
     CK(hipDeviceSynchronize());
-    CK(hipMemcpy(ref.data(), p.y, ny * 4, hipMemcpyDeviceToHost));
+    fetch(ref);
     for (size_t v = 1; v < kos.size(); ++v) {
       CK(hipMemset(p.y, 0, ny * 4));
       launch(kos[v]);
       CK(hipDeviceSynchronize());
-      CK(hipMemcpy(got.data(), p.y, ny * 4, hipMemcpyDeviceToHost));
+      fetch(got);
       size_t nd = 0;
       double md = 0;
       for (size_t i = 0; i < ny; ++i)
