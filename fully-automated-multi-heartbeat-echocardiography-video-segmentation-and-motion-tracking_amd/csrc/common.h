@@ -134,6 +134,8 @@ int winot_split_for(const ConvParams& p);
 void winot_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 // Patch-staged bf16 implicit GEMM for stride-1 1x3x3 and 3x1x1 convs (conv_patch.hip); p.w = conv_dma's
 // image.
+bool proj_x3_supported(const ConvParams& p);
+hipError_t launch_proj_x3(const ConvParams& p, hipStream_t s);
 bool patch_bf16_supported(const ConvParams& p);
 bool patch32_bf16_supported(const ConvParams& p);
 hipError_t launch_patch32_bf16(const ConvParams& p, hipStream_t s);

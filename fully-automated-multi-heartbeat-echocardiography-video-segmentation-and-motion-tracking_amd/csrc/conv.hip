@@ -507,6 +507,119 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
 }
 
 // ---------------------------------------------------------------------------------------------
+// conv_proj_x3 (round 4): the decoder's 1x1x1 tap projections (P01 = W0 f_stem + W1 f_layer1, P2,
+// P3: 64 output channels, K = 128 / 128 / 256) as a persistent split-bf16 GEMM. On conv_dma_x3 a
+// 128-voxel block ran only K / 32 = 4 ring steps, so its prologue and epilogue latencies dominated
+// (P01: 1.04 ms per 30 clips for 2.1 GB of traffic). Here each block DMAs W's three bf16 pieces to LDS
+// once and its waves walk 32-voxel items of the map, loading the next item's activations (fp32,
+// 16 B per lane and K block half) into registers while the current item's MFMAs run; the products,
+// their order and the epilogue are conv_dma_x3's (bit-identical output).
+//  * W image in LDS: [K/32][3 pieces][4 N tiles][16 rows][64 B], slot q of row r at q ^ G[r >> 2]
+//    (the weight image of dma_x3_weight_image, re-sliced by LDS-DMA);
+//  * item = 32 voxels (2 MFMA column blocks) x 64 channels: per K block 12 ds_read_b128, 8 f32x4
+//    activation loads per lane, 48 MFMAs of 16 cycles.
+template <int KB, int NB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv_proj_x3(ConvParams p, int n_items) {
+  constexpr int G[4] = {0, 2, 3, 1};
+  constexpr int PIECES = KB * 12;  // 1-KiB LDS pieces of W
+  __shared__ __align__(16) char smem[PIECES * 1024];
+  const float* x = reinterpret_cast<const float*>(p.x);
+  const float* x2 = reinterpret_cast<const float*>(p.x2);
+  const __bf16* w = reinterpret_cast<const __bf16*>(p.w);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, l16 = lane & 15;
+
+  // W: piece j = (kb, pc, nt) holds rows 16 nt .. +15 of piece pc of K block kb; lane -> row lane / 4,
+  // physical slot lane & 3 holding logical slot (lane & 3) ^ G[(row >> 2) & 3]
+  {
+    const int drow = lane >> 2, dq = (lane & 3) ^ G[(drow >> 2) & 3];
+    for (int j = wid; j < PIECES; j += 4) {
+      const int nt = j & 3, pc = (j >> 2) % 3, kb = j / 12;
+      const __bf16* src = w + ((size_t)(16 * nt + drow) * KB * 3 + (size_t)kb * 3 + pc) * 32 + 8 * dq;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(smem + j * 1024), 16, 0, 0);
+    }
+  }
+  const int b_off = l16 * 64 + (q ^ G[l16 >> 2]) * 16;
+
+  const int cin = p.Cin, cin2 = p.x2 ? p.Cin2 : 0;
+  // activations of item it: voxel m = 32 it + 16 i + l16, K block kb, 16-channel half h: channels
+  // 4q..4q+3 (conv_dma_x3's lane order); items past the end load nothing
+  auto load_item = [&](int it, f32x4 (&a)[KB][2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = 32 * it + 16 * i + l16;
+      const bool ok = it < n_items && m < p.M;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const bool second = 32 * kb >= cin;
+        const float* src = second ? x2 + (size_t)m * cin2 + (32 * kb - cin) : x + (size_t)m * cin + 32 * kb;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          if (ok) v = *reinterpret_cast<const f32x4*>(src + 16 * h + 4 * q);
+          a[kb][i][h] = v;
+        }
+      }
+    }
+  };
+  auto compute = [&](int it, const f32x4 (&a)[KB][2][2]) __attribute__((always_inline)) {
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) {
+      bf16x8 ah[2], am[2], al[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) split3_bf16x8(a[kb][i][0], a[kb][i][1], ah[i], am[i], al[i]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const char* st = smem + (kb * 12 + j) * 1024 + b_off;
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(st);
+        const bf16x8 bm = *reinterpret_cast<const bf16x8*>(st + 4 * 1024);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(st + 8 * 1024);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          f32x4 c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah[i], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al[i], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am[i], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah[i], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, am[i], c, 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah[i], c, 0, 0, 0);
+        }
+      }
+    }
+    epilogue<2, 4>(p, acc, 32 * it, 0, q, l16);
+  };
+
+  // NB register buffers: items it, it + S, .. it + (NB - 1) S in flight (S = waves in the grid);
+  // the loop is unrolled NB times so every buffer index is a compile-time register
+  const int S = gridDim.x * 4;
+  int it = blockIdx.x * 4 + wid;
+  f32x4 buf[NB][KB][2][2];
+#pragma unroll
+  for (int b = 0; b < NB - 1; ++b) load_item(it + b * S, buf[b]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the W DMAs landed
+  __syncthreads();
+  while (it < n_items) {
+    bool done = false;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (!done) {
+        load_item(it + (NB - 1) * S, buf[(b + NB - 1) % NB]);
+        compute(it, buf[b]);
+        it += S;
+        done = it >= n_items;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Register-staged variant for the stem's 1x7x7 conv over 3 (padded 4) fp32 input channels: the
 // 16-deep K slice spans 4 taps, decoded per float4. BM = 128, BN = 16*NT.
 template <int NT>
@@ -855,6 +968,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 }
 
 }  // namespace
+
+// conv_proj_x3: fp32 1x1x1 stride-1 convs to 64 channels over K = Cin (+ Cin2) = 128, both inputs
+// multiples of 32 channels, channels-last in and out, no split-K (the decoder projections P01 and P2;
+// K = 256 (P3) needs more registers than the item ring leaves and stays on conv_dma_x3)
+bool proj_x3_supported(const ConvParams& p) {
+  if (p.in_bf16 || p.out_bf16 || p.stem || p.x_c8 || p.y_c8 || p.n_split > 1) return false;
+  if (p.KT != 1 || p.KH != 1 || p.KW != 1 || p.st != 1 || p.sh != 1 || p.sw != 1) return false;
+  if (p.Cout != 64 || p.Cin % 32 || (p.x2 && p.Cin2 % 32)) return false;
+  const int k = p.Cin + (p.x2 ? p.Cin2 : 0);
+  if (p.Kp != k || k != 128) return false;
+  return (size_t)p.M * (p.Cin > 64 ? p.Cin : 64) < ((size_t)1 << 31);
+}
+
+// p.w: dma_x3_weight_image of the conv (the same image conv_dma_x3 reads)
+hipError_t launch_proj_x3(const ConvParams& p, hipStream_t s) {
+  if (!proj_x3_supported(p)) return hipErrorInvalidValue;
+  const int n_items = (p.M + 31) / 32;
+  const int kb = p.Kp / 32;
+  // persistent: one block (one wave per SIMD, 512 registers for the in-flight items) per CU, or
+  // fewer when the map is small
+  int blocks = 256;
+  if (blocks * 4 > n_items) blocks = (n_items + 3) / 4;
+  (void)kb;
+  hipLaunchKernelGGL((conv_proj_x3<4, 3>), dim3(blocks), dim3(256), 0, s, p, n_items);
+  return hipGetLastError();
+}
 
 // conv_dma_x3 (fp32 engines, non-stem implicit-GEMM convs): fp32 activations in, fp32 out
 bool dma_x3_supported(const ConvParams& p) {

@@ -121,6 +121,7 @@ int env_variants() {
   if (on("CLASFV_NO_STEM_X3")) f |= CLASFV_VARIANT_NO_STEM_X3;
   if (on("CLASFV_NO_WINO4W")) f |= CLASFV_VARIANT_NO_WINO4W;
   if (on("CLASFV_NO_PATCH32")) f |= CLASFV_VARIANT_NO_PATCH32;
+  if (on("CLASFV_NO_PROJ_X3")) f |= CLASFV_VARIANT_NO_PROJ_X3;
   return f;
 }
 
@@ -363,6 +364,8 @@ double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
                                 : (double)((out.h * out.w + 63) / 64 * 64);
     return 2.0 * out.n * ((out.t + fr - 1) / fr * fr) * px * c.cout_p * (double)c.Kp * 1e-9;
   }
+  if (!strcmp(kname, "conv_proj_x3"))  // 32-voxel items, the fp32 GEMM it computes
+    return 2.0 * ceil((double)out.n * out.t * out.h * out.w / 32.0) * 32.0 * c.cout_p * (double)c.Kp * 1e-9;
   if (!strcmp(kname, "conv_patch32_bf16"))  // 4 frames x 8x8-pixel tiles
     return 2.0 * out.n * ((out.t + 3) / 4 * 4) * (double)((out.h + 7) / 8 * 8) * ((out.w + 7) / 8 * 8) * c.cout_p *
            (double)c.Kp * 1e-9;
@@ -417,6 +420,7 @@ const char* pick_kernel(const Conv& c, ConvParams p) {
   if (c.dwinot && c.dx3 && (long)p.To * p.Ho * p.Wo <= 256 && !p.x_c8 && !p.y_c8 && dma_x3_supported(p))
     return "conv_dma_x3";
   if (c.dwinot && winot_supported(p)) return "conv_winot";
+  if (c.dx3 && !(p.vflags & CLASFV_VARIANT_NO_PROJ_X3) && proj_x3_supported(p)) return "conv_proj_x3";
   if (!(p.vflags & (CLASFV_VARIANT_NO_PATCH_BF16 | CLASFV_VARIANT_NO_PATCH32)) && patch32_bf16_supported(p))
     return "conv_patch32_bf16";
   if (!(p.vflags & CLASFV_VARIANT_NO_PATCH_BF16) && patch_bf16_supported(p)) return "conv_patch_bf16";
@@ -498,6 +502,9 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
     HIP_TRY(launch_patch_bf16(p, s));
   } else if (!strcmp(k, "conv_patch32_bf16")) {
     HIP_TRY(launch_patch32_bf16(p, s));
+  } else if (!strcmp(k, "conv_proj_x3")) {
+    p.w = c.dx3;
+    HIP_TRY(launch_proj_x3(p, s));
   } else if (!strcmp(k, "conv_dma_x3")) {
     p.w = c.dx3;
     const int S = dma_split_for(p, 2);
@@ -866,7 +873,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0x7FFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~0xFFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;

@@ -613,6 +613,24 @@ def test_wino4w_bitexact_vs_wino4(model, shape):
     assert torch.equal(s_w, s_4) and torch.equal(m_w, m_4)
 
 
+@pytest.mark.parametrize("shape", [(1, 3, 32, 112, 112), (2, 3, 16, 64, 48), (3, 3, 8, 32, 32)])
+def test_proj_x3_bitexact_vs_dma_x3(model, shape):
+    """The decoder's 128-deep tap projections (P01 = W0 f_stem + W1 f_layer1, P2) on the persistent
+    conv_proj_x3 (conv.hip) against conv_dma_x3 (variant no_proj_x3): the same six split-bf16 products
+    per 32-deep K block in the same order and the same epilogue, so the forward is bit-identical."""
+    rng = np.random.default_rng(59)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    model.engine.set_kernel_timing(True)
+    s_p, m_p = model(x)
+    kt = model.engine.kernel_timing()
+    model.engine.set_kernel_timing(False)
+    assert kt["conv_proj_x3"]["launches"] == 2  # P01 and P2
+    model.set_kernel_variants("no_proj_x3")
+    s_d, m_d = model(x)
+    model.set_kernel_variants()
+    assert torch.equal(s_p, s_d) and torch.equal(m_p, m_d)
+
+
 @pytest.mark.parametrize("shape", [(2, 3, 32, 112, 112), (3, 3, 24, 80, 112)])
 def test_bf16_patch32_bitexact_vs_patch16(shape):
     """config[4]: the bf16 layer1 spatial convs on conv_patch32_bf16 (v_mfma_f32_32x32x16_bf16, 4-frame
