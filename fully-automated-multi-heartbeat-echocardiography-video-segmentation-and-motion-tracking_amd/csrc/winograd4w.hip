@@ -62,7 +62,7 @@ constexpr int w4w_lds() {
 // C8: 8-channel-blocked output. DPW: DMA instructions per wave per chunk (W4Ring). KO: timing
 // knock-outs for tools/convbench (0 in the product; results are wrong otherwise): 1 no transform,
 // 2 no U loads in the loop, 4 no epilogue, 8 no DMAs in the loop, 128 the epilogue without its output
-// stores.
+// stores, 256 the serial (unpipelined) epilogue order.
 template <int NTN, bool C8, int DPW, int KO = 0>
 __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv_wino4w(ConvParams p,
                                                                                                       W4Geo g) {
@@ -276,9 +276,7 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
   const bool ulive = utile < NT && uxx < W;
   const int eb = ub == 3 ? 1 : ub;
   const int CO = p.Cout;
-#pragma unroll
-  for (int nt = 0; nt < NTN; ++nt) {
-    __builtin_amdgcn_sched_barrier(0);  // one N tile's accumulators at a time (no hoisted AGPR reads)
+  auto write_planes = [&](int nt) __attribute__((always_inline)) {
     float* Z = Z0 + (nt & 1) * W4W_ZBUF;
     if (ch == 0) {
 #pragma unroll
@@ -301,37 +299,66 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
         zp[3 * W4W_ZP / 4] = 8.f * df + m2;
       }
     }
-    __syncthreads();
-    if (ulive) {
-      f32x4 P[6];
+  };
+  auto read_unit = [&](int nt, f32x4 (&P)[6]) __attribute__((always_inline)) {
+    const float* Z = Z0 + (nt & 1) * W4W_ZBUF;
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
-        P[i] = *reinterpret_cast<const f32x4*>(Z + (i * 3 + eb) * W4W_ZP + utile * W4W_ZT + 4 * ucq) +
-               *reinterpret_cast<const f32x4*>(Z + (18 + i * 4 + ub) * W4W_ZP + utile * W4W_ZT + 4 * ucq);
-      const int co = (cob * NTN + nt) * 16 + 4 * ucq;
-      const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 s12 = P[1] + P[2], d12 = P[1] - P[2], s34 = P[3] + P[4], d34 = P[3] - P[4];
-      f32x4 y[4];
-      y[0] = P[0] + s12 + s34;
-      y[1] = d12 + 2.f * d34;
-      y[2] = s12 + 4.f * s34;
-      y[3] = d12 + 8.f * d34 + P[5];
+    for (int i = 0; i < 6; ++i)
+      P[i] = *reinterpret_cast<const f32x4*>(Z + (i * 3 + eb) * W4W_ZP + utile * W4W_ZT + 4 * ucq) +
+             *reinterpret_cast<const f32x4*>(Z + (18 + i * 4 + ub) * W4W_ZP + utile * W4W_ZT + 4 * ucq);
+  };
+  auto store_unit = [&](int nt, const f32x4 (&P)[6]) __attribute__((always_inline)) {
+    const int co = (cob * NTN + nt) * 16 + 4 * ucq;
+    const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 s12 = P[1] + P[2], d12 = P[1] - P[2], s34 = P[3] + P[4], d34 = P[3] - P[4];
+    f32x4 y[4];
+    y[0] = P[0] + s12 + s34;
+    y[1] = d12 + 2.f * d34;
+    y[2] = s12 + 4.f * s34;
+    y[3] = d12 + 8.f * d34 + P[5];
 #pragma unroll
-      for (int aa = 0; aa < 4; ++aa) {
-        if (4 * uty + aa >= H) break;  // partial tiles at the bottom edge (H % 4 != 0)
-        f32x4 o = y[aa] + bias;
-        if (p.relu) {
+    for (int aa = 0; aa < 4; ++aa) {
+      if (4 * uty + aa >= H) break;  // partial tiles at the bottom edge (H % 4 != 0)
+      f32x4 o = y[aa] + bias;
+      if (p.relu) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
-        }
-        const size_t pix = (size_t)(uf * H + 4 * uty + aa) * W + uxx;
-        const size_t off = C8 ? (size_t)(co >> 3) * plane + pix * 8 + (co & 7) : pix * CO + co;
-        if constexpr ((KO & 128) != 0) {  // probe: no output stores
-          if (o[0] == 1234.5f) *reinterpret_cast<f32x4*>(yout + off) = o;
-        } else {
-          *reinterpret_cast<f32x4*>(yout + off) = o;
-        }
+        for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
       }
+      const size_t pix = (size_t)(uf * H + 4 * uty + aa) * W + uxx;
+      const size_t off = C8 ? (size_t)(co >> 3) * plane + pix * 8 + (co & 7) : pix * CO + co;
+      if constexpr ((KO & 128) != 0) {  // probe: no output stores
+        if (o[0] == 1234.5f) *reinterpret_cast<f32x4*>(yout + off) = o;
+      } else {
+        *reinterpret_cast<f32x4*>(yout + off) = o;
+      }
+    }
+  };
+  if constexpr ((KO & 256) != 0) {
+    // the first round-4 form (timing reference): write, barrier, read / transform / store per N tile
+#pragma unroll
+    for (int nt = 0; nt < NTN; ++nt) {
+      __builtin_amdgcn_sched_barrier(0);
+      write_planes(nt);
+      __syncthreads();
+      if (ulive) {
+        f32x4 P[6];
+        read_unit(nt, P);
+        store_unit(nt, P);
+      }
+    }
+  } else {
+    // software-pipelined: N tile nt's plane reads are issued, then N tile nt + 1's planes are written
+    // into the other buffer (last read at nt - 1, before this iteration's barrier) while they are in
+    // flight, then nt's output transform and stores run
+    write_planes(0);
+#pragma unroll
+    for (int nt = 0; nt < NTN; ++nt) {
+      __builtin_amdgcn_sched_barrier(0);  // one N tile's accumulators at a time (no hoisted AGPR reads)
+      __syncthreads();
+      f32x4 P[6];
+      if (ulive) read_unit(nt, P);
+      if (nt + 1 < NTN) write_planes(nt + 1);
+      if (ulive) store_unit(nt, P);
     }
   }
 }
@@ -450,6 +477,7 @@ hipError_t launch_wino4w_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 8: return launch_w4w_dpw<9, 8>(p, g, nb, s);
     case 15: return launch_w4w_dpw<9, 15>(p, g, nb, s);
     case 128: return launch_w4w_dpw<9, 128>(p, g, nb, s);
+    case 256: return launch_w4w_dpw<9, 256>(p, g, nb, s);
     default: return launch_w4w_dpw<9>(p, g, nb, s);
   }
 }
