@@ -114,7 +114,8 @@ int main(int argc, char** argv) {
   p.Kp = bf ? (p.K + 31) / 32 * 32 : (p.K + 15) / 16 * 16;
   p.M = N * p.To * p.Ho * p.Wo;
   p.relu = 1;
-  if (getenv("CB_STAGGER")) p.patch_nt = atoi(getenv("CB_STAGGER"));  // conv_wino4w ko 64: sleep units per phase
+  if (getenv("CB_STAGGER")) p.patch_nt = atoi(getenv("CB_STAGGER"));
+  if (getenv("CB_C8") && winot) p.x_c8 = 1;  // 8-channel-blocked input (the engine's mid tensors)  // conv_wino4w ko 64: sleep units per phase
   const size_t nx = (size_t)N * T * H * W * Cin, ny = (size_t)p.M * Cout;
   p.x = bf ? to_bf16_dev(nx, 0.f, 1.f, 1) : dev_random(nx, 0.f, 1.f, 1);
   const size_t nw = wino4w ? wino4w_weight_floats(Cin, Cout) : wino4 ? (size_t)(Cout / 48) * (Cin / 8) * 14336 : winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
