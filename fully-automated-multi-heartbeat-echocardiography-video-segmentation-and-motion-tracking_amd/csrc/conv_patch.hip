@@ -86,7 +86,9 @@ __device__ inline void for_taps(std::integer_sequence<int, I...>, F&& f) {
 // register cap follow from it).
 // STG: LDS-staged output stores (the product form; false = 8-B stores from the accumulator layout,
 // convbench A/B)
-template <int NT, int KT, int FR, int S, int OCC, bool STG = true>
+// EF: epilogue flags at compile time, bit 0 residual, bit 1 ReLU (runtime flags kept both forms of every
+// epilogue statement in the code)
+template <int NT, int KT, int FR, int S, int OCC, bool STG = true, int EF = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void conv_patch_bf16(
     ConvParams p, int n_tiles, int ptw, int npt, int t_tiles) {
   using G = PGeo<KT, FR>;
@@ -254,11 +256,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     const int n = n0 + j * 16 + 4 * q;
     f32x4 v = acc[i][j];
     if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
-    if (res) {
+    if constexpr (EF & 1) {
       const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + gm * p.Cout + n);
       v += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
     }
-    if (p.relu) {
+    if constexpr (EF & 2) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
     }
@@ -288,8 +290,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     for (int i0 = 0; i0 < MT; i0 += MH) {
 #pragma unroll
       for (int i = i0; i < i0 + MH; ++i) {
-        size_t gm;
-        voxel(16 * (MT * wid + i) + l16, gm);
+        size_t gm = 0;
+        if constexpr (EF & 1) voxel(16 * (MT * wid + i) + l16, gm);
 #pragma unroll
         for (int j = 0; j < NT; ++j)
           *reinterpret_cast<bf16x4*>(st + (16 * (i - i0) + l16) * VS + (16 * j + 4 * q) * 2) = finish(i, j, gm);
@@ -297,12 +299,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the pass's 16 MH voxels: block voxel mp + v (v < 16 MH), frame f = mp >> 6 of the block, pixel
+      // px0 + v of its 64 (spatial: rows px0 / 8 + v / 8 of the 8x8 tile, column v % 8); store
+      // addresses = a wave-uniform base + a small per-lane offset, masks only on edge tiles
+      const int mp = 16 * (MT * wid + i0), f = mp >> 6, px0 = mp & 63, to = t0 + f;
+      __bf16* yb;
+      bool full;
+      int row_el = 0;
+      if constexpr (G::SPATIAL) {
+        yb = y + ((((size_t)clip * p.To + to) * p.Ho + h0 + px0 / 8) * p.Wo + w0) * p.Cout + n0;
+        full = to < p.To && h0 + px0 / 8 + 2 * MH <= p.Ho && w0 + 8 <= p.Wo;
+        row_el = p.Wo * p.Cout;
+      } else {
+        yb = y + (((size_t)clip * p.To + to) * HW + hw0 + px0) * p.Cout + n0;
+        full = to < p.To && hw0 + px0 + 16 * MH <= HW;
+      }
 #pragma unroll
       for (int k = 0; k < INS; ++k) {
         const int e = 1024 * k + 16 * lane, v = e / SEG, off = e - v * SEG;
         const bf16x8 val = *reinterpret_cast<const bf16x8*>(st + v * VS + off);
-        size_t gm;
-        if (voxel(16 * (MT * wid + i0) + v, gm)) *reinterpret_cast<bf16x8*>(y + gm * p.Cout + n0 + off / 2) = val;
+        const int lo = G::SPATIAL ? (v >> 3) * row_el + (v & 7) * p.Cout + off / 2 : v * p.Cout + off / 2;
+        bool ok = full;
+        if (!full) {
+          if constexpr (G::SPATIAL) ok = to < p.To && h0 + px0 / 8 + (v >> 3) < p.Ho && w0 + (v & 7) < p.Wo;
+          else ok = to < p.To && hw0 + px0 + v < HW;
+        }
+        if (ok) *reinterpret_cast<bf16x8*>(yb + lo) = val;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -336,13 +358,23 @@ PatchGrid patch_grid(const ConvParams& p, int fr) {
   return g;
 }
 
-template <int NT, int KT, int FR, int S = 3, bool STG = true>
-hipError_t launch_p(const ConvParams& p, hipStream_t s) {
+template <int NT, int KT, int FR, int S, bool STG, int EF>
+hipError_t launch_pe(const ConvParams& p, hipStream_t s) {
   const PatchGrid g = patch_grid(p, FR);
   const int n_tiles = p.Cout / (16 * NT);
-  hipLaunchKernelGGL((conv_patch_bf16<NT, KT, FR, S, patch_occ<NT, KT, FR, S>(), STG>), dim3((unsigned)(g.base * n_tiles)),
+  hipLaunchKernelGGL((conv_patch_bf16<NT, KT, FR, S, patch_occ<NT, KT, FR, S>(), STG, EF>), dim3((unsigned)(g.base * n_tiles)),
                      dim3(256), 0, s, p, n_tiles, g.ptw, g.npt, g.tt);
   return hipGetLastError();
+}
+
+template <int NT, int KT, int FR, int S = 3, bool STG = true>
+hipError_t launch_p(const ConvParams& p, hipStream_t s) {
+  switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
+    case 0: return launch_pe<NT, KT, FR, S, STG, 0>(p, s);
+    case 1: return launch_pe<NT, KT, FR, S, STG, 1>(p, s);
+    case 2: return launch_pe<NT, KT, FR, S, STG, 2>(p, s);
+    default: return launch_pe<NT, KT, FR, S, STG, 3>(p, s);
+  }
 }
 
 // Output frames per block and B ring depth (tools/bench_patch.sh): 1x3x3 convs 2 frames, 2 stages
@@ -590,15 +622,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   const __bf16* res = reinterpret_cast<const __bf16*>(p.res);
   __bf16* y = reinterpret_cast<__bf16*>(p.y);
   const int to = t0 + wid;
+  // epilogue flags at compile time (MODE 256: residual, 512: ReLU): a runtime flag left both forms of
+  // every statement in the code, and their address arithmetic outweighed the main loop's VALU
+  constexpr bool RES = (MODE & 256) != 0, RELU = (MODE & 512) != 0;
   auto finish = [&](int rb, int cb, int g, size_t gm) __attribute__((always_inline)) {
     const int n = n0 + 32 * rb + 8 * g + 4 * h;
     f32x4 v = {acc[rb][cb][4 * g], acc[rb][cb][4 * g + 1], acc[rb][cb][4 * g + 2], acc[rb][cb][4 * g + 3]};
     if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
-    if (res) {
+    if constexpr (RES) {
       const bf16x4 rv = *reinterpret_cast<const bf16x4*>(res + gm * p.Cout + n);
       v += f32x4{(float)rv[0], (float)rv[1], (float)rv[2], (float)rv[3]};
     }
-    if (p.relu) {
+    if constexpr (RELU) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
     }
@@ -628,15 +663,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     // LDS-staged stores: a lane's 8-B pieces are scattered over 32 voxels (32 partial lines per store
     // instruction); staged through the dead patch buffers as [32 voxels][NB*64 B + 16], each column
     // block leaves as NB*2 16-B-per-lane stores of whole voxel segments (contiguous 8-pixel rows
-    // when the block covers every channel)
+    // when the block covers every channel). Store addresses: a wave-uniform base (clip, frame, first
+    // row of the column block) plus a small per-lane offset.
     constexpr int SEG = NB * 64, VS = SEG + 16, INS = SEG * 32 / 1024;
     static_assert(4 * 32 * VS <= 2 * PBYTES, "staging fits the patch buffers");
     char* st = smem + wid * 32 * VS;
+    const bool full = to < p.To && h0 + 8 <= p.Ho && w0 + 8 <= p.Wo;  // wave-uniform
+    const int row_el = p.Wo * p.Cout;                                 // elements per map row
     __builtin_amdgcn_s_barrier();  // every wave is past its last patch / weight read
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       const int ho_l = h0 + 4 * cb + (vox >> 3), wo_l = w0 + (vox & 7);
-      const size_t gm_l = (((size_t)clip * p.To + to) * p.Ho + (ho_l < p.Ho ? ho_l : 0)) * p.Wo + (wo_l < p.Wo ? wo_l : 0);
+      size_t gm_l = 0;
+      if constexpr (RES)
+        gm_l = (((size_t)clip * p.To + (to < p.To ? to : 0)) * p.Ho + (ho_l < p.Ho ? ho_l : 0)) * p.Wo +
+               (wo_l < p.Wo ? wo_l : 0);
 #pragma unroll
       for (int rb = 0; rb < NB; ++rb)
 #pragma unroll
@@ -645,17 +686,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __bf16* yb = y + ((((size_t)clip * p.To + to) * p.Ho + h0 + 4 * cb) * p.Wo + w0) * p.Cout + n0;
 #pragma unroll
       for (int k = 0; k < INS; ++k) {
         const int e = 1024 * k + 16 * lane, v = e / SEG, off = e - v * SEG;
         const bf16x8 val = *reinterpret_cast<const bf16x8*>(st + v * VS + off);
-        const int ho = h0 + 4 * cb + (v >> 3), wo = w0 + (v & 7);
-        if (to < p.To && ho < p.Ho && wo < p.Wo) {
-          const size_t gm = (((size_t)clip * p.To + to) * p.Ho + ho) * p.Wo + wo;
+        const int r = v >> 3, c = v & 7;
+        __bf16* dst = yb + (r * row_el + c * p.Cout + off / 2);
+        if (full || (to < p.To && h0 + 4 * cb + r < p.Ho && w0 + c < p.Wo)) {
           if constexpr (MODE & 64) {
-            __builtin_nontemporal_store(val, reinterpret_cast<bf16x8*>(y + gm * p.Cout + n0 + off / 2));
+            __builtin_nontemporal_store(val, reinterpret_cast<bf16x8*>(dst));
           } else {
-            *reinterpret_cast<bf16x8*>(y + gm * p.Cout + n0 + off / 2) = val;
+            *reinterpret_cast<bf16x8*>(dst) = val;
           }
         }
       }
@@ -673,13 +715,24 @@ constexpr int patch32_occ() {
   return occ > 4 ? 4 : occ;
 }
 
-template <int NB, int S = 2, int EPI = 1>
-hipError_t launch_p32(const ConvParams& p, hipStream_t s) {
+template <int NB, int S, int MODE>
+hipError_t launch_p32_m(const ConvParams& p, hipStream_t s) {
   const PatchGrid g = patch_grid(p, 4);
   const int n_tiles = p.Cout / (32 * NB);
-  hipLaunchKernelGGL((conv_patch32_bf16<NB, S, patch32_occ<NB, S>(), EPI>), dim3((unsigned)(g.base * n_tiles)), dim3(256), 0,
-                     s, p, n_tiles, g.ptw, g.npt, g.tt);
+  hipLaunchKernelGGL((conv_patch32_bf16<NB, S, patch32_occ<NB, S>(), MODE>), dim3((unsigned)(g.base * n_tiles)), dim3(256),
+                     0, s, p, n_tiles, g.ptw, g.npt, g.tt);
   return hipGetLastError();
+}
+
+// EPI: MODE bits 0..6 (1 = the staged product epilogue); the residual / ReLU bits come from p
+template <int NB, int S = 2, int EPI = 1>
+hipError_t launch_p32(const ConvParams& p, hipStream_t s) {
+  switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
+    case 0: return launch_p32_m<NB, S, EPI>(p, s);
+    case 1: return launch_p32_m<NB, S, EPI | 256>(p, s);
+    case 2: return launch_p32_m<NB, S, EPI | 512>(p, s);
+    default: return launch_p32_m<NB, S, EPI | 768>(p, s);
+  }
 }
 
 // N tile (32-channel blocks). Product rule: NB = 5 (160-channel blocks: the bf16 layer1 spatial
