@@ -6,6 +6,22 @@
 #include "clasfv.h"
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// ReLU in one instruction, bit-identical to fmaxf(x, 0.f) for every non-NaN x (-0 and negatives give
+// +0): fmaxf compiles to two v_max_f32 (an IEEE canonicalisation of x, then the max)
+__device__ inline float relu1(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+
+// a - b on 4 floats as two packed adds with the second operand negated (exactly a - b per lane): the
+// compiler emits four scalar v_sub_f32 for the vector subtraction
+__device__ inline f32x4 psub4(f32x4 a, f32x4 b) {
+  const f32x2 alo = {a[0], a[1]}, ahi = {a[2], a[3]}, blo = {b[0], b[1]}, bhi = {b[2], b[3]};
+  f32x2 lo, hi;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(lo) : "v"(alo), "v"(blo));
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(hi) : "v"(ahi), "v"(bhi));
+  return f32x4{lo[0], lo[1], hi[0], hi[1]};
+}
+
 
 // n / d for a runtime divisor d >= 1 and n < 2^31 as one multiply-high and an add (Granlund-Montgomery
 // with a 33-bit multiplier): a per-lane integer division by a kernel argument is a ~30-instruction

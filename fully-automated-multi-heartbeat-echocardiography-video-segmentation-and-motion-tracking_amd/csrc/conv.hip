@@ -96,7 +96,7 @@ __device__ inline void epilogue(const ConvParams& p, const f32x4 (&acc)[MT][NT],
       f32x4 v = acc[i][j] + bv + rv;
       if (p.relu) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.f);
+        for (int c = 0; c < 4; ++c) v[c] = relu1(v[c]);
       }
       store_out4(p.y, o, v, p.out_bf16);
     }
@@ -828,7 +828,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         const int n = 16 * j + 4 * q;
         f32x4 v = acc[i][j] + *reinterpret_cast<const f32x4*>(p.bias + n);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        for (int e = 0; e < 4; ++e) v[e] = relu1(v[e]);
         *reinterpret_cast<bf16x4*>(y + m * 64 + n) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
       }
     }
@@ -1109,7 +1109,7 @@ __global__ __launch_bounds__(256) void split_sum_kernel(const float* __restrict_
   if (res) v += reinterpret_cast<const f32x4*>(res)[i];
   if (relu)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.f);
+    for (int c = 0; c < 4; ++c) v[c] = relu1(v[c]);
   reinterpret_cast<f32x4*>(y)[i] = v;
 }
 

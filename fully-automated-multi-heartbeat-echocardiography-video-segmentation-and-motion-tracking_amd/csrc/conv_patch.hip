@@ -262,7 +262,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     }
     if constexpr (EF & 2) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      for (int e = 0; e < 4; ++e) v[e] = relu1(v[e]);
     }
     return bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
   };
@@ -635,7 +635,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     }
     if constexpr (RELU) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      for (int e = 0; e < 4; ++e) v[e] = relu1(v[e]);
     }
     return bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
   };

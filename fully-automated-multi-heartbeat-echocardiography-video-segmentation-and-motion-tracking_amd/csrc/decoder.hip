@@ -170,7 +170,7 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
         a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh_[kb], hh[mt][kb], a, 0, 0, 0);
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) a[r] = fmaxf(a[r], 0.f);
+      for (int r = 0; r < 4; ++r) a[r] = relu1(a[r]);
       acc[mt][nt] = a;  // h2^T[ch = 16nt + 4q + r][voxel l16]
     }
   }
@@ -406,7 +406,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ?
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) h1[mt][c][j] = fmaxf(h1[mt][c][j], 0.f);
+      for (int j = 0; j < 4; ++j) h1[mt][c][j] = relu1(h1[mt][c][j]);
 
   if constexpr (BF) {
     decoder_heads_bf16<MODE == 4, true>(p, h1, t, n, h0, w0, wid, q, l16);
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ?
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[mt][nt][r] = fmaxf(acc[mt][nt][r], 0.f);
+      for (int r = 0; r < 4; ++r) acc[mt][nt][r] = relu1(acc[mt][nt][r]);
 #pragma unroll
     for (int c = 0; c < 4; ++c) wa[c] = wn[c];
   }

@@ -307,7 +307,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           const float y = a == 0 ? z[0][h][e] + z[1][h][e] + z[2][h][e] : z[1][h][e] - z[2][h][e] - z[3][h][e];
           float o = y + u_b[u][c];
           if (res) o += u_r[u][px][c];
-          if (p.relu) o = fmaxf(o, 0.f);
+          if (p.relu) o = relu1(o);
           v[c] = o;
         }
         *reinterpret_cast<f32x4*>(yout + u_o[u] + (size_t)(a * W + b) * CO) = v;

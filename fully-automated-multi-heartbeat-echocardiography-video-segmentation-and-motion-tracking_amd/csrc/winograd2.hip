@@ -356,7 +356,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           const float y = a2 == 0 ? z[0][h][e] + z[1][h][e] + z[2][h][e] : z[1][h][e] - z[2][h][e] - z[3][h][e];
           float o = y + u_b[u][c];
           if constexpr (RES) o += u_r[u][2 * a2 + b2][c];
-          if constexpr (RELU) o = fmaxf(o, 0.f);
+          if constexpr (RELU) o = relu1(o);
           v[c] = o;
         }
         *reinterpret_cast<f32x4*>(yout + u_o[u] + (size_t)(a2 * W + b2) * ps) = v;

@@ -320,7 +320,7 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int aa = 0; aa < 4; ++aa) {
           if (4 * vty + aa >= H) break;
           float o = y[aa][tt] + bias;
-          if constexpr (RELU) o = fmaxf(o, 0.f);
+          if constexpr (RELU) o = relu1(o);
           const size_t pix = (size_t)(vf * H + 4 * vty + aa) * W + vxx;
           yout[C8 ? (size_t)(co >> 3) * plane + pix * 8 + (co & 7) : pix * CO + co] = o;
         }
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         f32x4 o = y[aa] + bias;
         if constexpr (RELU) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
+          for (int c = 0; c < 4; ++c) o[c] = relu1(o[c]);
         }
         const size_t pix = (size_t)(uf * H + 4 * uty + aa) * W + uxx;
         const size_t off = C8 ? (size_t)(co >> 3) * plane + pix * 8 + (co & 7) : pix * CO + co;

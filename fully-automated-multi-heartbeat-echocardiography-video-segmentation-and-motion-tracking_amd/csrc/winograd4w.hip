@@ -63,7 +63,7 @@ constexpr int w4w_lds() {
 // knock-outs for tools/convbench (0 in the product; results are wrong otherwise): 1 no transform,
 // 2 no U loads in the loop, 4 no epilogue, 8 no DMAs in the loop, 128 the epilogue without its output
 // stores, 256 the serial (unpipelined) epilogue order.
-template <int NTN, bool C8, int DPW, int KO = 0>
+template <int NTN, bool C8, int DPW, int KO = 0, bool RELU = true>
 __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv_wino4w(ConvParams p,
                                                                                                       W4Geo g) {
   using RG = W4Ring<DPW>;
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
         const f32x4 m0 = acc[nt][r][0], m1 = acc[nt][r][1], m2 = acc[nt][r][2];
         f32x4* zp = reinterpret_cast<f32x4*>(Z + ((3 * rh + r) * 3) * W4W_ZP + l16 * W4W_ZT + 4 * q);
         zp[0] = m0 + m1 + m2;
-        zp[W4W_ZP / 4] = m1 - m2;
+        zp[W4W_ZP / 4] = psub4(m1, m2);
         zp[2 * W4W_ZP / 4] = m1 + m2;
       }
     } else {
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
       for (int r = 0; r < 3; ++r) {
         const f32x4 m0 = acc[nt][r][0], m1 = acc[nt][r][1], m2 = acc[nt][r][2];
         f32x4* zp = reinterpret_cast<f32x4*>(Z + (18 + (3 * rh + r) * 4) * W4W_ZP + l16 * W4W_ZT + 4 * q);
-        const f32x4 sm = m0 + m1, df = m0 - m1;
+        const f32x4 sm = m0 + m1, df = psub4(m0, m1);
         zp[0] = sm;
         zp[W4W_ZP / 4] = 2.f * df;
         zp[2 * W4W_ZP / 4] = 4.f * sm;
@@ -307,10 +307,20 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
       P[i] = *reinterpret_cast<const f32x4*>(Z + (i * 3 + eb) * W4W_ZP + utile * W4W_ZT + 4 * ucq) +
              *reinterpret_cast<const f32x4*>(Z + (18 + i * 4 + ub) * W4W_ZP + utile * W4W_ZT + 4 * ucq);
   };
+  // output addresses: the thread's 4 pixel rows aa at N tile 0, then a uniform stride per N tile
+  const int co0 = cob * NTN * 16 + 4 * ucq;
+  const size_t upix = (size_t)(uf * H + 4 * uty) * W + uxx;
+  float* ybase[4];
+#pragma unroll
+  for (int aa = 0; aa < 4; ++aa) {
+    const size_t px = upix + (size_t)aa * W;
+    ybase[aa] = yout + (C8 ? (size_t)(co0 >> 3) * plane + px * 8 + (co0 & 7) : px * CO + co0);
+  }
+  const size_t nt_step = C8 ? 2 * plane : 16;  // co + 16 per N tile
   auto store_unit = [&](int nt, const f32x4 (&P)[6]) __attribute__((always_inline)) {
-    const int co = (cob * NTN + nt) * 16 + 4 * ucq;
+    const int co = co0 + nt * 16;
     const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const f32x4 s12 = P[1] + P[2], d12 = P[1] - P[2], s34 = P[3] + P[4], d34 = P[3] - P[4];
+    const f32x4 s12 = P[1] + P[2], d12 = psub4(P[1], P[2]), s34 = P[3] + P[4], d34 = psub4(P[3], P[4]);
     f32x4 y[4];
     y[0] = P[0] + s12 + s34;
     y[1] = d12 + 2.f * d34;
@@ -320,16 +330,15 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
     for (int aa = 0; aa < 4; ++aa) {
       if (4 * uty + aa >= H) break;  // partial tiles at the bottom edge (H % 4 != 0)
       f32x4 o = y[aa] + bias;
-      if (p.relu) {
+      if constexpr (RELU) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) o[c] = fmaxf(o[c], 0.f);
+        for (int c = 0; c < 4; ++c) o[c] = relu1(o[c]);
       }
-      const size_t pix = (size_t)(uf * H + 4 * uty + aa) * W + uxx;
-      const size_t off = C8 ? (size_t)(co >> 3) * plane + pix * 8 + (co & 7) : pix * CO + co;
+      float* dst = ybase[aa] + nt * nt_step;
       if constexpr ((KO & 128) != 0) {  // probe: no output stores
-        if (o[0] == 1234.5f) *reinterpret_cast<f32x4*>(yout + off) = o;
+        if (o[0] == 1234.5f) *reinterpret_cast<f32x4*>(dst) = o;
       } else {
-        *reinterpret_cast<f32x4*>(yout + off) = o;
+        *reinterpret_cast<f32x4*>(dst) = o;
       }
     }
   };
@@ -376,10 +385,15 @@ int wino4w_ntn(int cout) {
 template <int NTN, int DPW, int KO = 0>
 hipError_t launch_w4w(const ConvParams& p, const W4Geo& g, int n_blocks, hipStream_t s) {
   const dim3 grid(n_blocks), block(W4_THREADS);
-  if (p.y_c8)
-    hipLaunchKernelGGL((conv_wino4w<NTN, true, DPW, KO>), grid, block, 0, s, p, g);
+  // every Conv2Plus1D spatial half is followed by BN + ReLU: the ReLU form is the one that runs
+  if (p.y_c8 && p.relu)
+    hipLaunchKernelGGL((conv_wino4w<NTN, true, DPW, KO, true>), grid, block, 0, s, p, g);
+  else if (p.relu)
+    hipLaunchKernelGGL((conv_wino4w<NTN, false, DPW, KO, true>), grid, block, 0, s, p, g);
+  else if (p.y_c8)
+    hipLaunchKernelGGL((conv_wino4w<NTN, true, DPW, KO, false>), grid, block, 0, s, p, g);
   else
-    hipLaunchKernelGGL((conv_wino4w<NTN, false, DPW, KO>), grid, block, 0, s, p, g);
+    hipLaunchKernelGGL((conv_wino4w<NTN, false, DPW, KO, false>), grid, block, 0, s, p, g);
   return hipGetLastError();
 }
 

@@ -232,7 +232,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3, 3))) vo
         f32x4 v = yv[a2] + bv[u] + rv[u][a2];
         if (p.relu) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.f);
+          for (int c = 0; c < 4; ++c) v[c] = relu1(v[c]);
         }
         *reinterpret_cast<f32x4*>(yout + o0[u] + a2 * fstride) = v;
       }
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         rv[a2] = ((EPI & 1) && ok) ? *reinterpret_cast<const f32x4*>(res + o + a2 * fstride) : f32x4{0.f, 0.f, 0.f, 0.f};
       const f32x4 m0 = acc[0][m][nt], m1 = acc[1][m][nt], m2 = acc[2][m][nt], m3 = acc[3][m][nt],
                   m4 = acc[4][m][nt], m5 = acc[5][m][nt];
-      const f32x4 s12 = m1 + m2, d12 = m1 - m2, s34 = m3 + m4, d34 = m3 - m4;
+      const f32x4 s12 = m1 + m2, d12 = psub4(m1, m2), s34 = m3 + m4, d34 = psub4(m3, m4);
       f32x4 yv[4];
       yv[0] = m0 + s12 + s34;
       yv[1] = d12 + 2.f * d34;
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           if constexpr (EPI & 1) vv += rv[a2];
           if constexpr (EPI & 2) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) vv[c] = fmaxf(vv[c], 0.f);
+            for (int c = 0; c < 4; ++c) vv[c] = relu1(vv[c]);
           }
           *reinterpret_cast<f32x4*>(yout + o + a2 * fstride) = vv;
         }
