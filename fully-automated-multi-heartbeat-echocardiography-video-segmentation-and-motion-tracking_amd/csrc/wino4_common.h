@@ -90,36 +90,53 @@ __device__ inline void bt_cols(const f32x2 (&t)[6], f32x2 (&v)[3]) {
 // Tile-group shape, patch pitches and DMA count for p with output-channel blocks of cob_w channels
 // (false: no group of >= 12 tiles fits). Tiles
 // past the map's right / bottom edge (H, W % 4 != 0) are computed on zero padding and not stored.
-inline bool wino4_geometry(const ConvParams& p, W4Geo* g, int* n_blocks, int cob_w = 48) {
+// fill16 (conv_wino4w): among the (TR, TC) shapes take the one with the most tiles (16 fills every MFMA
+// row), then the widest; otherwise the widest TC first (the least halo per tile: conv_wino4's rule).
+// At 56x56 maps (TW = 14) that is 8 rows x 2 tiles instead of 1 x 14: 16 of 16 MFMA rows carry tiles
+// instead of 14, for 20 % more raw-patch bytes per tile.
+inline bool wino4_geometry(const ConvParams& p, W4Geo* g, int* n_blocks, int cob_w = 48, bool fill16 = false) {
   if (p.Cout % cob_w || p.Cin % 8) return false;
   const int TH = (p.Ho + 3) / 4, TW = (p.Wo + 3) / 4;
   const long rows = (long)p.N * p.To * TH;  // flattened tile rows
+  // TR divides one clip's tile rows (To * TH), not the batch's: the group shape -- and so whether this
+  // kernel runs at all, and every clip's rounding -- depends on the per-clip shape only, never on N
+  auto tr_for = [&](int tc) {
+    for (int d = 16 / tc; d >= 1; --d)
+      if (((long)p.To * TH) % d == 0) return d;
+    return 1;
+  };
+  // RP, SS for a (TR, TC): fewest tiles sharing a 16-B bank quad of a 256-B row (ds_read_b64: a 32-lane
+  // group = 16 tiles x one channel pair), then the 4-stage ring (<= 16 DMA instructions), then the
+  // fewest DMAs; false when no pitch keeps a chunk within 24 DMA instructions
+  auto pitch = [&](int TR, int TC) {
+    const int PC = 4 * TC + 2, rp0 = (PC - 1) + (PC - 1) / 4 + 1;
+    int best = 1 << 30;
+    for (int rp = rp0; rp < rp0 + 16; ++rp)
+      for (int ss = 6 * rp; ss < 6 * rp + 16; ++ss) {
+        const int ni = (2 * TR * ss + 63) / 64;
+        if (ni > W4_WAVES * 6) continue;
+        int cnt[16] = {0}, m = 0;
+        for (int t = 0; t < TR * TC; ++t) {
+          const int v = ((t / TC) * ss + 5 * (t % TC)) & 15;
+          if (++cnt[v] > m) m = cnt[v];
+        }
+        const int score = m * 1000 + (ni <= 16 ? 0 : 100) + ni;
+        if (score < best) best = score, g->RP = rp, g->SS = ss;
+      }
+    return best != (1 << 30);
+  };
+  // candidates: the widest TC (conv_wino4's rule), and with fill16 the most tiles per group (TC >= 2)
   int TC = 0;
   for (int d = TW < 16 ? TW : 16; d >= 1 && !TC; --d)
     if (TW % d == 0) TC = d;
-  // TR divides one clip's tile rows (To * TH), not the batch's: the group shape -- and so whether this
-  // kernel runs at all, and every clip's rounding -- depends on the per-clip shape only, never on N
-  int TR = 0;
-  for (int d = 16 / TC; d >= 1 && !TR; --d)
-    if (((long)p.To * TH) % d == 0) TR = d;
-  if (TR * TC < 12) return false;
-  const int PC = 4 * TC + 2, rp0 = (PC - 1) + (PC - 1) / 4 + 1;
-  // RP, SS: fewest tiles sharing a 16-B bank quad of a 256-B row (ds_read_b64: a 32-lane group = 16
-  // tiles x one channel pair), then the 4-stage ring (<= 16 DMA instructions), then the fewest DMAs
-  int best = 1 << 30;
-  for (int rp = rp0; rp < rp0 + 16; ++rp)
-    for (int ss = 6 * rp; ss < 6 * rp + 16; ++ss) {
-      const int ni = (2 * TR * ss + 63) / 64;
-      if (ni > W4_WAVES * 6) continue;
-      int cnt[16] = {0}, m = 0;
-      for (int t = 0; t < TR * TC; ++t) {
-        const int v = ((t / TC) * ss + 5 * (t % TC)) & 15;
-        if (++cnt[v] > m) m = cnt[v];
-      }
-      const int score = m * 1000 + (ni <= 16 ? 0 : 100) + ni;
-      if (score < best) best = score, g->RP = rp, g->SS = ss;
-    }
-  if (best == 1 << 30) return false;
+  int TR = tr_for(TC);
+  if (fill16) {
+    int bc = TC, br = TR;
+    for (int d = TW < 16 ? TW : 16; d >= 2; --d)
+      if (TW % d == 0 && tr_for(d) * d > br * bc) bc = d, br = tr_for(d);
+    if ((bc != TC || br != TR) && br * bc >= 12 && pitch(br, bc)) TC = bc, TR = br;
+  }
+  if (TR * TC < 12 || !pitch(TR, TC)) return false;
   g->TR = TR, g->TC = TC, g->TH = TH, g->TW = TW;
   g->RS = TR * g->SS;
   g->NI = (2 * g->RS + 63) / 64;

@@ -414,7 +414,7 @@ bool wino4w_supported(const ConvParams& p) {
          p.sh == 1 && p.sw == 1 && p.st == 1 && p.ph == 1 && p.pw == 1 && p.pt == 0 && p.Ho == p.Hi &&
          p.Wo == p.Wi && p.To == p.Ti &&
          (size_t)p.N * p.To * p.Ho * p.Wo * (p.Cin > p.Cout ? p.Cin : p.Cout) < ((size_t)1 << 31) &&
-         wino4_geometry(p, &g, &nb, 16 * ntn);
+         wino4_geometry(p, &g, &nb, 16 * ntn, true);
 }
 
 // p.w: wino4w_transform_weights' layout for this Cout's NTN.
@@ -423,7 +423,7 @@ hipError_t launch_wino4w(const ConvParams& p, hipStream_t s) {
   W4Geo g;
   int nb;
   const int ntn = wino4w_ntn(p.Cout);
-  wino4_geometry(p, &g, &nb, 16 * ntn);
+  wino4_geometry(p, &g, &nb, 16 * ntn, true);
   return ntn == 9 ? launch_w4w_dpw<9>(p, g, nb, s) : launch_w4w_dpw<6>(p, g, nb, s);
 }
 
@@ -432,7 +432,7 @@ double wino4w_exec_gflop(const ConvParams& p) {
   W4Geo g;
   int nb;
   const int ntn = wino4w_ntn(p.Cout);
-  return ntn && wino4_geometry(p, &g, &nb, 16 * ntn) ? 2.0 * nb * 16.0 * 36.0 * p.Cin * 16.0 * ntn * 1e-9 : 0.0;
+  return ntn && wino4_geometry(p, &g, &nb, 16 * ntn, true) ? 2.0 * nb * 16.0 * 36.0 * p.Cin * 16.0 * ntn * 1e-9 : 0.0;
 }
 
 // Floats of wino4w_transform_weights' output for a cin_p x cout_p conv (0: no wide block fits).
@@ -478,12 +478,14 @@ void wino4w_transform_weights(const double* w, int cout, int cin, int cout_p, in
 }
 
 #ifdef CLASFV_KNOCKOUTS
-// tools/convbench: conv_wino4w timing knock-outs (KO bits above).
+// tools/convbench: conv_wino4w timing knock-outs (KO bits above; 1024: conv_wino4's tile-group rule).
 hipError_t launch_wino4w_ko(const ConvParams& p, hipStream_t s, int ko) {
   if (!wino4w_supported(p) || wino4w_ntn(p.Cout) != 9) return hipErrorInvalidValue;
   W4Geo g;
   int nb;
-  wino4_geometry(p, &g, &nb, 144);
+  // ko 1024 + bits: the widest-TC tile groups (conv_wino4's shape rule) instead of 16-tile groups
+  wino4_geometry(p, &g, &nb, 144, !(ko & 1024));
+  ko &= ~1024;
   switch (ko) {
     case 1: return launch_w4w_dpw<9, 1>(p, g, nb, s);
     case 2: return launch_w4w_dpw<9, 2>(p, g, nb, s);
