@@ -94,7 +94,7 @@ __device__ inline void bt_cols(const f32x2 (&t)[6], f32x2 (&v)[3]) {
 // row), then the widest; otherwise the widest TC first (the least halo per tile: conv_wino4's rule).
 // At 56x56 maps (TW = 14) that is 8 rows x 2 tiles instead of 1 x 14: 16 of 16 MFMA rows carry tiles
 // instead of 14, for 20 % more raw-patch bytes per tile.
-inline bool wino4_geometry(const ConvParams& p, W4Geo* g, int* n_blocks, int cob_w = 48, bool fill16 = false) {
+inline bool wino4_geometry(const ConvParams& p, W4Geo* g, int* n_blocks, int cob_w = 48, int fill16 = 0) {
   if (p.Cout % cob_w || p.Cin % 8) return false;
   const int TH = (p.Ho + 3) / 4, TW = (p.Wo + 3) / 4;
   const long rows = (long)p.N * p.To * TH;  // flattened tile rows
@@ -125,14 +125,15 @@ inline bool wino4_geometry(const ConvParams& p, W4Geo* g, int* n_blocks, int cob
       }
     return best != (1 << 30);
   };
-  // candidates: the widest TC (conv_wino4's rule), and with fill16 the most tiles per group (TC >= 2)
+  // candidates: the widest TC (conv_wino4's rule), and with fill16 the most tiles per group among
+  // TC >= fill16
   int TC = 0;
   for (int d = TW < 16 ? TW : 16; d >= 1 && !TC; --d)
     if (TW % d == 0) TC = d;
   int TR = tr_for(TC);
   if (fill16) {
     int bc = TC, br = TR;
-    for (int d = TW < 16 ? TW : 16; d >= 2; --d)
+    for (int d = TW < 16 ? TW : 16; d >= fill16; --d)
       if (TW % d == 0 && tr_for(d) * d > br * bc) bc = d, br = tr_for(d);
     if ((bc != TC || br != TR) && br * bc >= 12 && pitch(br, bc)) TC = bc, TR = br;
   }

@@ -391,13 +391,17 @@ hipError_t launch_w4(const ConvParams& p, const W4Geo& g, int n_blocks, hipStrea
 
 }  // namespace
 
+// tile groups: the most tiles per group (16 fills every MFMA row), then the widest (28x28 maps: 16 x 1
+// instead of 2 x 7); wino4_geometry
+constexpr int W4_FILL = 1;
+
 bool wino4_supported(const ConvParams& p) {
   W4Geo g;
   int nb;
   return !p.in_bf16 && !p.out_bf16 && !p.stem && !p.x2 && !p.res && p.KT == 1 && p.KH == 3 && p.KW == 3 &&
          p.sh == 1 && p.sw == 1 && p.st == 1 && p.ph == 1 && p.pw == 1 && p.pt == 0 && p.Ho == p.Hi &&
          p.Wo == p.Wi && p.To == p.Ti && (size_t)p.N * p.To * p.Ho * p.Wo * (p.Cin > p.Cout ? p.Cin : p.Cout) <
-         ((size_t)1 << 31) && wino4_geometry(p, &g, &nb);
+         ((size_t)1 << 31) && wino4_geometry(p, &g, &nb, 48, W4_FILL);
 }
 
 // p.w: wino4_transform_weights' layout. (The launch templates are called from this non-template
@@ -406,7 +410,7 @@ hipError_t launch_wino4(const ConvParams& p, hipStream_t s) {
   if (!wino4_supported(p)) return hipErrorInvalidValue;
   W4Geo g;
   int nb;
-  wino4_geometry(p, &g, &nb);
+  wino4_geometry(p, &g, &nb, 48, W4_FILL);
   const int dpw = (g.NI + W4_WAVES - 1) / W4_WAVES;
   switch (p.Cin >> 3) {
     case 8:
@@ -423,7 +427,7 @@ hipError_t launch_wino4(const ConvParams& p, hipStream_t s) {
 double wino4_exec_gflop(const ConvParams& p) {
   W4Geo g;
   int nb;
-  return wino4_geometry(p, &g, &nb) ? 2.0 * nb * 16.0 * 36.0 * p.Cin * 48.0 * 1e-9 : 0.0;
+  return wino4_geometry(p, &g, &nb, 48, W4_FILL) ? 2.0 * nb * 16.0 * 36.0 * p.Cin * 48.0 * 1e-9 : 0.0;
 }
 
 // U[cout_p/48][cin_p/8][4 waves][14][64 lane][4] from folded weights w[cout][cin][3][3] (double): wave
@@ -477,7 +481,7 @@ static hipError_t launch_w4ko(const ConvParams& p, const W4Geo& g, int nb, hipSt
 hipError_t launch_wino4_ko(const ConvParams& p, hipStream_t s, int ko) {
   W4Geo g;
   int nb;
-  if (!wino4_supported(p) || (p.Cin != 64 && p.Cin != 128) || p.y_c8 || !p.relu || !wino4_geometry(p, &g, &nb) ||
+  if (!wino4_supported(p) || (p.Cin != 64 && p.Cin != 128) || p.y_c8 || !p.relu || !wino4_geometry(p, &g, &nb, 48, W4_FILL) ||
       g.NI > 16)
     return hipErrorInvalidValue;
   switch (ko) {

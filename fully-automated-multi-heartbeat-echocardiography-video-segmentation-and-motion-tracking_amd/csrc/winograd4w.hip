@@ -372,6 +372,11 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
   }
 }
 
+// tile groups: the most tiles per group (16 fills every MFMA row), then the widest, among column
+// widths >= W4W_FILL (56x56 maps: 8 x 2 tiles, 28x28: 16 x 1)
+// (profiles/r04_wino4w_fill16.txt)
+constexpr int W4W_FILL = 1;
+
 // NTN for a Cout: the widest of 9, 6 N tiles dividing it (0: none). NTN = 5 (layer2's 240 channels)
 // compiles but ran 0.785 vs conv_wino4's 0.754 ms (r04b): the 80-channel block pays the one-wave-per-SIMD
 // serialisation without enough reuse to win it back, so conv_wino4 keeps that conv.
@@ -414,7 +419,7 @@ bool wino4w_supported(const ConvParams& p) {
          p.sh == 1 && p.sw == 1 && p.st == 1 && p.ph == 1 && p.pw == 1 && p.pt == 0 && p.Ho == p.Hi &&
          p.Wo == p.Wi && p.To == p.Ti &&
          (size_t)p.N * p.To * p.Ho * p.Wo * (p.Cin > p.Cout ? p.Cin : p.Cout) < ((size_t)1 << 31) &&
-         wino4_geometry(p, &g, &nb, 16 * ntn, true);
+         wino4_geometry(p, &g, &nb, 16 * ntn, W4W_FILL);
 }
 
 // p.w: wino4w_transform_weights' layout for this Cout's NTN.
@@ -423,7 +428,7 @@ hipError_t launch_wino4w(const ConvParams& p, hipStream_t s) {
   W4Geo g;
   int nb;
   const int ntn = wino4w_ntn(p.Cout);
-  wino4_geometry(p, &g, &nb, 16 * ntn, true);
+  wino4_geometry(p, &g, &nb, 16 * ntn, W4W_FILL);
   return ntn == 9 ? launch_w4w_dpw<9>(p, g, nb, s) : launch_w4w_dpw<6>(p, g, nb, s);
 }
 
@@ -432,7 +437,7 @@ double wino4w_exec_gflop(const ConvParams& p) {
   W4Geo g;
   int nb;
   const int ntn = wino4w_ntn(p.Cout);
-  return ntn && wino4_geometry(p, &g, &nb, 16 * ntn, true) ? 2.0 * nb * 16.0 * 36.0 * p.Cin * 16.0 * ntn * 1e-9 : 0.0;
+  return ntn && wino4_geometry(p, &g, &nb, 16 * ntn, W4W_FILL) ? 2.0 * nb * 16.0 * 36.0 * p.Cin * 16.0 * ntn * 1e-9 : 0.0;
 }
 
 // Floats of wino4w_transform_weights' output for a cin_p x cout_p conv (0: no wide block fits).
@@ -483,9 +488,10 @@ hipError_t launch_wino4w_ko(const ConvParams& p, hipStream_t s, int ko) {
   if (!wino4w_supported(p) || wino4w_ntn(p.Cout) != 9) return hipErrorInvalidValue;
   W4Geo g;
   int nb;
-  // ko 1024 + bits: the widest-TC tile groups (conv_wino4's shape rule) instead of 16-tile groups
-  wino4_geometry(p, &g, &nb, 144, !(ko & 1024));
-  ko &= ~1024;
+  // ko 1024 + bits: the widest-TC tile groups (conv_wino4's shape rule) instead of 16-tile groups;
+  // 2048 + bits: 16-tile groups down to one tile column
+  wino4_geometry(p, &g, &nb, 144, (ko & 1024) ? 0 : (ko & 2048) ? 1 : W4W_FILL);
+  ko &= ~3072;
   switch (ko) {
     case 1: return launch_w4w_dpw<9, 1>(p, g, nb, s);
     case 2: return launch_w4w_dpw<9, 2>(p, g, nb, s);
