@@ -79,8 +79,14 @@ __device__ inline void store_out4(void* y, size_t o, f32x4 v, int bf16) {
 // acc[i][j] (D^T layout): lane (l16, q) holds channels n0 + 16j + 4q .. +3 of voxel m_base + 16i + l16.
 // Cout is a multiple of 16, so a 4-channel group is either all inside or all outside. Each lane
 // reads its residual vector before writing the same addresses (res may alias y).
-template <int MT, int NT>
+// EF >= 0: the flags at compile time (bit 0 residual, 1 ReLU, 2 8-channel-blocked output; fp32 out),
+// so only one form of each statement is in the code; EF < 0: read from p.
+template <int MT, int NT, int EF = -1>
 __device__ inline void epilogue(const ConvParams& p, const f32x4 (&acc)[MT][NT], int m_base, int n0, int q, int l16) {
+  const bool has_res = EF < 0 ? p.res != nullptr : (EF & 1) != 0;
+  const bool relu = EF < 0 ? p.relu != 0 : (EF & 2) != 0;
+  const bool c8 = EF < 0 ? p.y_c8 != 0 : (EF & 4) != 0;
+  const int obf = EF < 0 ? p.out_bf16 : 0;
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int m = m_base + i * 16 + l16;
@@ -90,15 +96,15 @@ __device__ inline void epilogue(const ConvParams& p, const f32x4 (&acc)[MT][NT],
       const int n = n0 + j * 16 + 4 * q;
       if (n >= p.Cout) continue;
       // channels-last, or 8-channel blocks [Cout/8][M][8] (p.y_c8, fp32)
-      const size_t o = p.y_c8 ? ((size_t)(n >> 3) * p.M + m) * 8 + (n & 7) : (size_t)m * p.Cout + n;
+      const size_t o = c8 ? ((size_t)(n >> 3) * p.M + m) * 8 + (n & 7) : (size_t)m * p.Cout + n;
       const f32x4 bv = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 rv = p.res ? load_res4(p.res, o, p.out_bf16) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 rv = has_res ? load_res4(p.res, o, obf) : f32x4{0.f, 0.f, 0.f, 0.f};
       f32x4 v = acc[i][j] + bv + rv;
-      if (p.relu) {
+      if (relu) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = relu1(v[c]);
       }
-      store_out4(p.y, o, v, p.out_bf16);
+      store_out4(p.y, o, v, obf);
     }
   }
 }
@@ -326,7 +332,7 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
 // operands from its f32x4 slot of each step -- the same k set on both sides of the product.
 // WN: waves along N (1: 4 waves x (BM/4 rows x BN); 2: 2 x 2 waves of (BM/2 rows x BN/2), halving the
 // B-piece LDS reads per wave at twice the A splits).
-template <int MT, int NT, int S, int WN = 1>
+template <int MT, int NT, int S, int WN = 1, int EF = -1>
 __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, DmaDivs dv) {
   static_assert(NT % WN == 0, "N tiles split evenly over the waves along N");
   constexpr int MTW = MT * WN, NTW = NT / WN;  // 16 x 16 tiles per wave
@@ -503,7 +509,7 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
     partial_store<MTW, NTW>(p, acc, p.part + (size_t)split * p.M * p.Cout, m0 + wm * 16 * MTW, n0 + wn * 16 * NTW, q,
                             l16);
   else
-    epilogue<MTW, NTW>(p, acc, m0 + wm * 16 * MTW, n0 + wn * 16 * NTW, q, l16);
+    epilogue<MTW, NTW, EF>(p, acc, m0 + wm * 16 * MTW, n0 + wn * 16 * NTW, q, l16);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -852,7 +858,15 @@ hipError_t launch_dma_x3_t(const ConvParams& p, hipStream_t s) {
   const int mt = (p.M + BM - 1) / BM, nt = (p.Cout + BN - 1) / BN;
   const DmaDivs dv{fast_div(p.Wo), fast_div(p.Ho), fast_div(p.To), fast_div(nt)};
   const int n_split = p.n_split > 1 ? p.n_split : 1;
-  hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN>), dim3(mt * nt * n_split), dim3(256), 0, s, p, nt, dv);
+  const dim3 grid(mt * nt * n_split);
+  // the epilogue flags at compile time (split-K partials ignore them)
+  switch (n_split > 1 ? 0 : (p.res ? 1 : 0) | (p.relu ? 2 : 0) | (p.y_c8 ? 4 : 0)) {
+    case 0: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 0>), grid, dim3(256), 0, s, p, nt, dv); break;
+    case 1: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 1>), grid, dim3(256), 0, s, p, nt, dv); break;
+    case 2: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 2>), grid, dim3(256), 0, s, p, nt, dv); break;
+    case 3: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 3>), grid, dim3(256), 0, s, p, nt, dv); break;
+    default: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN>), grid, dim3(256), 0, s, p, nt, dv); break;
+  }
   if (n_split > 1) return launch_split_sum(p, s);
   return hipGetLastError();
 }
