@@ -1057,6 +1057,12 @@ hipError_t launch_dma_x3_cfg(const ConvParams& p, int mt, int nt, int S, hipStre
     case 263: return launch_dma_x3_t<2, 6, 3>(p, s);
     case 432: return launch_dma_x3_t<4, 3, 2>(p, s);
     case 462: return launch_dma_x3_t<4, 6, 2>(p, s);
+    case 152: return launch_dma_x3_t<1, 5, 2>(p, s);
+    case 452: return launch_dma_x3_t<4, 5, 2>(p, s);
+    case 253: return launch_dma_x3_t<2, 5, 3>(p, s);
+    case 442: return launch_dma_x3_t<4, 4, 2>(p, s);
+    case 482: return launch_dma_x3_t<4, 8, 2>(p, s);
+    case 182: return launch_dma_x3_t<1, 8, 2>(p, s);
   }
   return launch_dma_x3(p, 16 * nt, s);
 }
