@@ -339,6 +339,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int j = 0; j < DMAX; ++j) {
       if (j == DMIN && !more) break;  // wave-uniform
       const int I = wid + 4 * j;
+      if constexpr ((EPI & 4096) != 0) if (I >= G::RAW_I) continue;  // knock-out: no U DMAs
+      if constexpr ((EPI & 8192) != 0) if (I < G::RAW_I) continue;   // knock-out: no raw DMAs
       const char* src = (I < G::RAW_I ? xk : uk) + d_off[j];
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(smem + stage * G::STAGE + I * 1024), 16,
@@ -369,7 +371,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __builtin_amdgcn_sched_barrier(0);
   for (int k = k0; k < k1; ++k) {
     // (EPI >= 256: convbench timing knock-outs, results wrong: 256 no transform VALU, 512 no DMAs in
-    // the loop, 1024 no epilogue, 2048 no wait / barrier)
+    // the loop, 1024 no epilogue, 2048 no wait / barrier, 4096 no U DMAs, 8192 no raw DMAs)
     if constexpr ((EPI & 2048) == 0) {
       __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): chunk k's DMAs (own) landed
       __builtin_amdgcn_sched_barrier(0);
@@ -622,6 +624,10 @@ hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 804: return winot5_launch_e<4, 4, 2 + 1024>(p, s);
     case 808: return winot5_launch_e<4, 4, 2 + 2048>(p, s);
     case 815: return winot5_launch_e<4, 4, 2 + 256 + 512 + 1024 + 2048>(p, s);
+    case 816: return winot5_launch_e<4, 4, 2 + 4096>(p, s);   // no U DMAs in the loop
+    case 832: return winot5_launch_e<4, 4, 2 + 8192>(p, s);   // no raw DMAs in the loop
+    case 817: return winot5_launch_e<4, 4, 3 + 4096>(p, s);   // (residual form)
+    case 833: return winot5_launch_e<4, 4, 3 + 8192>(p, s);
     case 502: return winot5_dispatch(p, s, 2);
     case 504: return winot5_dispatch(p, s, 4);
   }
