@@ -70,6 +70,21 @@ __global__ void build_clips_kernel(const float* __restrict__ video, int T, int H
   if (resample) L = lin_ac_false(tk, tc, tf);
   const float* a = vc + (size_t)(shift + (resample ? L.i0 : tf)) * HW;
   const float* b = vc + (size_t)(shift + (resample ? L.i1 : tf)) * HW;
+  if ((HW & 3) == 0 && (((uintptr_t)video | (uintptr_t)clips) & 15) == 0) {  // 16-B vectors, the same per-element arithmetic
+    const f32x4* a4 = reinterpret_cast<const f32x4*>(a);
+    const f32x4* b4 = reinterpret_cast<const f32x4*>(b);
+    f32x4* o4 = reinterpret_cast<f32x4*>(out);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (HW >> 2); i += gridDim.x * blockDim.x) {
+      f32x4 v = a4[i];
+      if (resample) {
+        const f32x4 w = b4[i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = lerp_t(v[e], w[e], L.l0, L.l1);
+      }
+      o4[i] = v;
+    }
+    return;
+  }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += gridDim.x * blockDim.x)
     out[i] = resample ? lerp_t(a[i], b[i], L.l0, L.l1) : a[i];
 }
@@ -106,6 +121,36 @@ __global__ void pass_labels_kernel(const float* __restrict__ logits, PassTable t
   const float* b = base + (size_t)(L.i1 >> 5) * clip_stride + (size_t)(L.i1 & 31) * HW;
   const size_t cs = (size_t)32 * HW;  // class stride inside a clip
   uint8_t* out = labels + ((size_t)k * T + f) * HW;
+  if ((HW & 3) == 0 && ((uintptr_t)logits & 15) == 0 && ((uintptr_t)labels & 3) == 0) {
+    // 4 pixels per thread: 16-B logit loads, one 4-byte label store
+    auto lab = [&](float xa0, float xa1, float xb0, float xb1) __attribute__((always_inline)) {
+      float pa0, pa1;
+      softmax2(xa0, xa1, pa0, pa1);
+      float q0 = pa0, q1 = pa1;
+      if (resample) {
+        float pb0, pb1;
+        softmax2(xb0, xb1, pb0, pb1);
+        q0 = lerp_t(pa0, pb0, L.l0, L.l1);
+        q1 = lerp_t(pa1, pb1, L.l0, L.l1);
+      }
+      return (unsigned)(q1 > q0 ? 1 : 0);  // np.argmax: first maximum wins ties
+    };
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (HW >> 2); i += gridDim.x * blockDim.x) {
+      const f32x4 a0 = reinterpret_cast<const f32x4*>(a)[i];
+      const f32x4 a1 = MARGIN ? a0 : reinterpret_cast<const f32x4*>(a + cs)[i];
+      f32x4 b0 = a0, b1 = a1;
+      if (resample) {
+        b0 = reinterpret_cast<const f32x4*>(b)[i];
+        b1 = MARGIN ? b0 : reinterpret_cast<const f32x4*>(b + cs)[i];
+      }
+      unsigned w = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        w |= (MARGIN ? lab(0.f, a0[e], 0.f, b0[e]) : lab(a0[e], a1[e], b0[e], b1[e])) << (8 * e);
+      reinterpret_cast<unsigned*>(out)[i] = w;
+    }
+    return;
+  }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < HW; i += gridDim.x * blockDim.x) {
     float pa0, pa1;
     if (MARGIN)
@@ -717,7 +762,7 @@ inline int blocks_for(size_t n, int per_block, int cap) {
 
 hipError_t launch_build_clips(const float* video, int T, int HW, const int32_t* table, int n, int interp, float* clips,
                               hipStream_t s) {
-  dim3 grid(blocks_for(HW, 256, 64), 3 * 32, n);
+  dim3 grid(blocks_for(HW % 4 ? HW : HW / 4, 256, 64), 3 * 32, n);
   hipLaunchKernelGGL(build_clips_kernel, grid, dim3(256), 0, s, video, T, HW, table, interp, clips);
   return hipGetLastError();
 }
@@ -726,7 +771,7 @@ hipError_t launch_pass_labels(const float* logits, int K, const int32_t* clip0, 
                               int margin, uint8_t* labels, hipStream_t s) {
   PassTable tab;
   for (int k = 0; k < K; ++k) tab.clip0[k] = clip0[k];
-  dim3 grid(blocks_for(HW, 256, 64), T, K);
+  dim3 grid(blocks_for(HW % 4 ? HW : HW / 4, 256, 64), T, K);
   if (margin)
     hipLaunchKernelGGL(pass_labels_kernel<true>, grid, dim3(256), 0, s, logits, tab, T, step, HW, interp, labels);
   else
