@@ -911,14 +911,21 @@ hipError_t launch_bf16_m4(const ConvParams& p, int bn, hipStream_t s) {
 // conv_dma_x3, fp32 accumulation, 48 output channels (45 + 3 zero), fp32 output through the shared
 // epilogue (channels-last or 8-channel-blocked for the temporal Winograd after it). Weights: hi, mid
 // and lo images [48][7 kh][8 kw][4 c] bf16 (engine.hip, clasfv_finalize).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_stem_x3(ConvParams p) {
+// Persistent over 256-voxel items (n_items): the three weight images are staged in LDS once per block
+// and XCD x's blocks walk its contiguous item range with a stride of the blocks per XCD (gridDim.x % 8
+// == 0), the one-item form's dispatch order.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_stem_x3(ConvParams p, int n_items) {
   constexpr int MT = 4, NT = 3, CO = 16 * NT, ROW = 7 * 64, IMG = CO * ROW;
   __shared__ __align__(16) char ws[3 * IMG];  // hi, mid, lo images
   const float* x = reinterpret_cast<const float*>(p.x);
   const char* w16 = reinterpret_cast<const char*>(p.w);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int q = lane >> 4, l16 = lane & 15;
-  const int m0 = xcd_swizzle(blockIdx.x, gridDim.x) * 256 + wid * 64;
+  const int q8 = n_items >> 3, r8 = n_items & 7, x8 = blockIdx.x & 7;
+  const int i_start = x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8;
+  const int i_end = i_start + q8 + (x8 < r8 ? 1 : 0);
+  const int i_step = gridDim.x >> 3;
+  if (i_start + (int)(blockIdx.x >> 3) >= i_end) return;  // block-uniform, before the barrier
   for (int e = tid; e < 3 * CO * 28; e += 256) {  // [img][co][kh][slot] 16-B pieces, slot ^ (co & 3)
     const int im = e / (CO * 28), r0 = e - im * (CO * 28);
     const int co = r0 / 28, r = r0 - co * 28, kh = r >> 2, sl = r & 3;
@@ -927,6 +934,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   }
   __syncthreads();
   const int b_rd = l16 * ROW + ((q ^ (l16 & 3)) << 4);
+#pragma unroll 1
+  for (int item = i_start + (int)(blockIdx.x >> 3); item < i_end; item += i_step) {
+  const int m0 = item * 256 + wid * 64;
   const float* rowp[MT];
   int hi0[MT], wi0[MT];
   bool live[MT];
@@ -979,6 +989,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     }
   }
   epilogue<MT, NT>(p, acc, m0, 0, q, l16);
+  }  // items
 }
 
 }  // namespace
@@ -1197,7 +1208,10 @@ bool stem_x3_supported(const ConvParams& p) {
 // p.w: hi, mid, lo images, each [48][7 kh][8 kw][4 c] bf16 (engine.hip, clasfv_finalize).
 hipError_t launch_stem_x3(const ConvParams& p, hipStream_t s) {
   if (!stem_x3_supported(p)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv_stem_x3, dim3((p.M + 255) / 256), dim3(256), 0, s, p);
+  // two blocks per CU (64.5 KiB of weight images each), or one item per block on small maps
+  const int n_items = (int)((p.M + 255) / 256);
+  const int grid = n_items >= 1024 ? 512 : (n_items + 7) / 8 * 8;
+  hipLaunchKernelGGL(conv_stem_x3, dim3(grid), dim3(256), 0, s, p, n_items);
   return hipGetLastError();
 }
 

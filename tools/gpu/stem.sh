@@ -1,5 +1,5 @@
 #!/bin/bash
-# conv_stem_x3 with the next tap row prefetched:
+# conv_stem_x3 variants (persistent over 256-voxel items):
 # forward tests, then a bench line and a kernel trace. usage: bash tools/gpu/stem.sh OUTDIR
 out=${1:-gpurun_out/stem}; mkdir -p $out; export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu.py -x -v --timeout 120 --timeout-method thread -k "stem or forward_full or golden or batch_is_per_clip or config3 or x3" > $out/pytest.log 2>&1 || { echo "tests failed"; tail -40 $out/pytest.log; exit 1; }
