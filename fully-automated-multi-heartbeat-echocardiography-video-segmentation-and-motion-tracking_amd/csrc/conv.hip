@@ -740,24 +740,28 @@ __global__ __launch_bounds__(256) void conv_stem_f32(ConvParams p, int n_tiles) 
 //    stride-2 7x7 windows of neighbouring voxels overlap ~12x);
 //  * the hi and lo 64 x 224 weight images (2 x 28 KB) are staged in LDS once per block, 16-B slots
 //    swizzled by the row (conflict-free ds_read_b128);
-//  * block = 4 waves x 4 m tiles = 256 output voxels x 64 channels per pass, STEM_GROUPS passes per
-//    block (the 56 KB weight staging amortised over 1024 voxels); D^T = W . A^T, so the epilogue
-//    (folded-BN bias, ReLU) stores 8-B bf16 vectors of 4 consecutive channels.
-constexpr int STEM_GROUPS = 1;
+//  * block = 4 waves x 4 m tiles = 256 output voxels x 64 channels per item; persistent (round 4): two
+//    blocks per CU stage the 56 KB of weight images once and walk their XCD's contiguous item range
+//    (as conv_stem_x3); D^T = W . A^T, so the epilogue (folded-BN bias, ReLU) stores 8-B bf16 vectors
+//    of 4 consecutive channels.
 
 __device__ inline bf16x8 stem_bf16x8(f32x4 a, f32x4 b) {
   return bf16x8{(__bf16)a[0], (__bf16)a[1], (__bf16)a[2], (__bf16)a[3],
                 (__bf16)b[0], (__bf16)b[1], (__bf16)b[2], (__bf16)b[3]};
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_stem_bf16(ConvParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv_stem_bf16(ConvParams p, int n_items) {
   constexpr int MT = 4, NT = 4, ROW = 7 * 64, IMG = 64 * ROW;  // LDS weight row: 7 K steps x 64 B
   __shared__ __align__(16) char ws[2 * IMG];                    // hi image, lo image
   const float* x = reinterpret_cast<const float*>(p.x);
   const char* w16 = reinterpret_cast<const char*>(p.w);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int q = lane >> 4, l16 = lane & 15;
-  const int mb = xcd_swizzle(blockIdx.x, gridDim.x) * 256 * STEM_GROUPS + wid * 64;
+  const int q8 = n_items >> 3, r8 = n_items & 7, x8 = blockIdx.x & 7;  // gridDim.x % 8 == 0
+  const int i_start = x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8;
+  const int i_end = i_start + q8 + (x8 < r8 ? 1 : 0);
+  const int i_step = gridDim.x >> 3;
+  if (i_start + (int)(blockIdx.x >> 3) >= i_end) return;  // block-uniform, before the barrier
   for (int e = tid; e < 2 * 64 * 28; e += 256) {  // [img][co][kh][slot] 16-B pieces, slot ^ (co & 3)
     const int im = e / (64 * 28), r0 = e - im * (64 * 28);
     const int co = r0 / 28, r = r0 - co * 28, kh = r >> 2, sl = r & 3;
@@ -766,8 +770,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   }
   __syncthreads();
   const int b_rd = l16 * ROW + ((q ^ (l16 & 3)) << 4);
-  for (int g = 0; g < STEM_GROUPS; ++g) {
-    const int m0 = mb + g * 256;
+#pragma unroll 1
+  for (int item = i_start + (int)(blockIdx.x >> 3); item < i_end; item += i_step) {
+    const int m0 = item * 256 + wid * 64;
     // per m tile: input row of kh = 0 and the lane's first column (taps 2q, 2q+1)
     const float* rowp[MT];
     int hi0[MT], wi0[MT];
@@ -790,7 +795,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 1
     for (int kh = 0; kh < 7; ++kh) {
       bf16x8 ah[MT], al[MT], bh[NT], bl[NT];
 #pragma unroll
@@ -1218,7 +1223,9 @@ hipError_t launch_stem_x3(const ConvParams& p, hipStream_t s) {
 // p.w: hi then lo image, each [64][7 kh][8 kw][4 c] bf16 (engine.hip, clasfv_finalize).
 hipError_t launch_stem_bf16(const ConvParams& p, hipStream_t s) {
   if (!stem_bf16_supported(p)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv_stem_bf16, dim3((p.M + 256 * STEM_GROUPS - 1) / (256 * STEM_GROUPS)), dim3(256), 0, s, p);
+  const int n_items = (int)((p.M + 255) / 256);
+  const int grid = n_items >= 1024 ? 512 : (n_items + 7) / 8 * 8;
+  hipLaunchKernelGGL(conv_stem_bf16, dim3(grid), dim3(256), 0, s, p, n_items);
   return hipGetLastError();
 }
 
