@@ -80,6 +80,12 @@ def parse(argv=None):
                          "batch of --c2-videos full videos sharded clip-wise over the ranks (strong scaling); "
                          "c3: only the config[3] forward")
     ap.add_argument("--c2-videos", type=int, default=64, help="videos in the config[2] batch")
+    ap.add_argument("--c2-lengths", default="equal", choices=["equal", "ragged"],
+                    help="config[2] video lengths: equal (--frames each) or ragged (seeded EchoNet-like 100-300 "
+                         "frames: videos straddle the ranks' clip blocks and the owner all_to_all moves margins)")
+    ap.add_argument("--extra-c2-ragged", type=int, default=1,
+                    help="c1 at N > 1: also time the ragged config[2] batch (f = 1) so the multi-GPU run measures "
+                         "the RCCL exchange; reported as 'c2_ragged'")
     ap.add_argument("--c2-extra-fuse", type=int, default=5,
                     help="c2: also time the same batch with this many shifted passes (0: off); reported as 'fuse_extra'")
     ap.add_argument("--master-port", type=int, default=0, help="rendezvous port of the self-launched ranks (0: free)")
@@ -150,20 +156,83 @@ def timed(fn, steps, warmup, engine, world, dev):
     return float(t.item()), kt, out
 
 
-def forward_stats(kt, clips, gflop_per_clip, peak):
+# The matrix pipe each kernel issues to, per engine dtype. The engine counts every kernel's issued work
+# in its own pipe's products (clasfv_kernel_timing xgflop): f32 MFMA products for the Winograd / f32
+# kernels, bf16 MFMA products for the split-bf16 ("x3": six products per fp32 product) and bf16 ones.
+BF16_PIPE = {"conv_dma_x3", "conv_stem_x3", "conv_proj_x3", "conv_stem_bf16", "conv_patch_bf16", "conv_patch32_bf16",
+             "decoder_kernel"}
+PIPE_PEAK = {"f32": FP32_PEAK_TFLOPS, "bf16": BF16_PEAK_TFLOPS}
+
+
+def pipe_of(kernel, engine_dtype):
+    if kernel in BF16_PIPE or (kernel == "conv_dma" and engine_dtype == "bf16"):
+        return "bf16"
+    return "f32"
+
+
+def pmc_mfma_busy(dtype):
+    """{kernel: (MFMA-pipe busy fraction, effective GHz)} from the newest committed
+    profiles/r*_clock_mfma_busy*.txt of this dtype (tools/clock_summary.py: SQ_VALU_MFMA_BUSY_CYCLES over
+    GRBM_GUI_ACTIVE / 8 x 1,024 SIMDs, one PMC pass), with the file name."""
+    import glob
+    import re
+    suffix = "" if dtype == "fp32" else "_" + dtype
+    files = [f for f in glob.glob(os.path.join(REPO, "profiles", f"r*_clock_mfma_busy{suffix}.txt"))
+             if dtype != "fp32" or re.search(r"_clock_mfma_busy\.txt$", f)]
+    if not files:
+        return {}, None
+    def tag(path):
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    f = sorted(files, key=tag)[-1]
+    out = {}
+    for ln in open(f).read().splitlines()[1:]:
+        parts = ln.split()
+        if len(parts) >= 5:
+            try:
+                out[parts[0]] = (float(parts[3]), float(parts[2]))
+            except ValueError:
+                pass
+    return out, os.path.basename(f)
+
+
+def kernel_table(kt, engine_dtype):
+    """Per kernel class: launches, summed ms, the work it issues on ITS matrix pipe (f32 or bf16) as a
+    rate and a fraction of that pipe's peak, the algorithmic (direct-convolution) rate, and the PMC
+    MFMA-busy fraction from the committed clock / busy summary."""
+    busy, src = pmc_mfma_busy(engine_dtype)
+    out = {}
+    for k, v in kt.items():
+        pipe = pipe_of(k, engine_dtype)
+        r = v["xgflop"] / max(v["ms"], 1e-9)
+        b = busy.get(k[:22])
+        out[k] = {"launches": v["launches"], "ms": round(v["ms"], 3), "pipe": pipe,
+                  "issued_tflops": round(r, 2), "issued_frac_of_pipe_peak": round(r / PIPE_PEAK[pipe], 4),
+                  "algorithmic_tflops": round(v["gflop"] / max(v["ms"], 1e-9), 2),
+                  "pmc_mfma_busy": b and b[0], "pmc_clock_ghz": b and b[1]}
+    return {"kernels": out, "pmc_source": src,
+            "note": "issued = products the kernel issues to the matrix pipe it runs on (f32: 157.3 TFLOP/s; "
+                    "bf16: 2.5 PFLOP/s dense; split-bf16 x3 kernels: 6 bf16 products per fp32 product) / its "
+                    "summed HIP-event time; pmc_mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (cycles x 1,024 SIMDs) "
+                    "from the committed profile pmc_source (null: kernel not in it)"}
+
+
+def forward_stats(kt, clips, gflop_per_clip, peak, engine_dtype="fp32"):
     ms = sum(v["ms"] for v in kt.values())
-    xg = sum(v["xgflop"] for v in kt.values())
     alg = gflop_per_clip * clips / (ms * 1e-3) / 1e3 if ms > 0 else 0.0
+    # time the matrix pipes would need at their peaks for the work issued, over the summed kernel time
+    pipe_ms = sum(v["xgflop"] / PIPE_PEAK[pipe_of(k, engine_dtype)] for k, v in kt.items())
     return {"forward_ms_per_clip": round(ms / max(clips, 1), 4), "kernel_ms_sum": round(ms, 3),
             "algorithmic_tflops": round(alg, 3), "algorithmic_frac": round(alg / peak, 4),
-            "issued_mfma_tflops": round(xg / max(ms, 1e-9), 3), "issued_mfma_frac": round(xg / max(ms, 1e-9) / peak, 4),
+            "mfma_pipe_time_frac": round(pipe_ms / max(ms, 1e-9), 4),
             "gflop_per_clip": gflop_per_clip,
             "note": "sum of the per-kernel HIP-event times of every clasfv_forward launch; the decoder "
                     "projections of the stem/layer1, layer2 and layer3 taps run on a side stream concurrently "
                     "with layer4, so their intervals overlap the layer4 launches' and the sum exceeds the "
                     "forwards' device time by about that overlap (rates over this sum are conservative); "
-                    "algorithmic = direct-convolution GFLOP of the graph (comb_1 commuted), issued = MFMA "
-                    "work executed"}
+                    "algorithmic = direct-convolution GFLOP of the graph (comb_1 commuted) over the " + str(peak) +
+                    " TFLOP/s peak of the engine dtype; mfma_pipe_time_frac = sum over kernels of (work issued "
+                    "/ the peak of the pipe it runs on) / the summed time"}
 
 
 def kernel_roofline(ktimes, peak, dtype):
@@ -176,6 +245,7 @@ def kernel_roofline(ktimes, peak, dtype):
     name, k = max(ktimes.items(), key=lambda kv: kv[1]["ms"])
     n = max(k["launches"], 1)
     tflops = k["xgflop"] / max(k["ms"], 1e-9)  # GFLOP/ms = TFLOP/s
+    peak = PIPE_PEAK[pipe_of(name, dtype.split("_")[0])]  # the peak of the pipe this kernel issues to
     tr = profiled_traffic(name, dtype)
     return {"bound": "mfma", "achieved": round(tflops, 3), "peak": peak, "unit": "TFLOP/s",
             "frac": round(tflops / peak, 4), "traffic": tr and tr["bytes_per_launch"],
@@ -186,7 +256,7 @@ def kernel_roofline(ktimes, peak, dtype):
             "traffic_source": tr and tr["source"],
             "note": "achieved = MFMA work issued (Winograd F(4x4,3x3): 36 of the 144 direct products per 4x4 "
                     "tile, 16-tile MFMA groups; F(2x2,3x3): 16 of 36 per 2x2 tile; F(4,3): 6 of 12 per 4 frames; "
-                    "padded channels and partial tiles counted; split-bf16 kernels: the fp32 GEMM they compute) / time; algorithmic_equiv_tflops = the direct-"
+                    "padded channels and partial tiles counted; split-bf16 kernels: their bf16 products, rated against the bf16 pipe) / time; algorithmic_equiv_tflops = the direct-"
                     "convolution FLOPs of the same launches / time"}
 
 
@@ -343,7 +413,7 @@ def c3_run(args, model, world, dev, steps, warmup):
     peak = BF16_PEAK_TFLOPS if eng.dtype == "bf16" else FP32_PEAK_TFLOPS
     return {"value": round(n / dt, 3), "unit": "64x224x224 clips/s", "ms_per_step": round(dt / steps * 1e3, 3),
             "clips_per_step": args.c3_batch * world,
-            "forward": forward_stats(kt, args.c3_batch * steps, GFLOP_PER_CLIP_C3, peak),
+            "forward": forward_stats(kt, args.c3_batch * steps, GFLOP_PER_CLIP_C3, peak, eng.dtype),
             "roofline": kernel_roofline(kt, peak, eng.dtype + "_c3"),  # no c3 PMC profile: traffic null
             "note": "BASELINE config[3]: (N,3,64,224,224) model forward (seg + motion), the reference's "
                     "forward signature; the CLI path is fixed at 112x112 (src/fuse_utils.py:22)"}
@@ -371,60 +441,89 @@ def make_videos(args, lengths, needed, dev):
     return out
 
 
-def run_c2(args, model, world, rank, dev):
-    """BASELINE config[2]: a fixed batch of full videos (64 x 200 frames) sharded clip-wise over the
-    ranks (strong scaling). f = 1: 384 clips; the fuse_extra run repeats it with f = 5 (1920 clips)."""
+def c2_lengths(args):
+    import clasfv_amd.synthetic as S
+    if args.c2_lengths == "ragged":
+        return S.echonet_like_lengths(args.c2_videos)
+    return [args.frames] * args.c2_videos
+
+
+def c2_measure(args, model, world, rank, dev, lengths, fuse, steps, warmup):
+    """One config[2]-style run: the batch of videos `lengths` sharded clip-wise over the ranks, fused on
+    each video's owner; the owner all_to_all (dist.exchange_to_owners) is timed with events on the
+    compute stream around the margin computation and the collective (max over ranks)."""
     from clasfv_amd import dist as D
     eng = model.engine
-    lengths = [args.frames] * args.c2_videos
     peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else FP32_PEAK_TFLOPS
+    needed = D.videos_needed(lengths, fuse, args.step, rank, world)
+    videos = make_videos(args, lengths, needed, dev)
+    plans, n_total = D.global_clip_plan(lengths, fuse, args.step)
+    lo, hi = D.shard_bounds(n_total, rank, world)
+    evs = []
 
-    def one(fuse, steps, warmup):
-        needed = D.videos_needed(lengths, fuse, args.step, rank, world)
-        videos = make_videos(args, lengths, needed, dev)
-        plans, n_total = D.global_clip_plan(lengths, fuse, args.step)
-        lo, hi = D.shard_bounds(n_total, rank, world)
+    def step():
+        return D.segment_videos_sharded(videos, model, num_clips=fuse, step=args.step,
+                                        fuse_method=args.fuse_method, rank=rank, world=world,
+                                        batch_size=args.batch_size, lengths=lengths, exchange_events=evs)
 
-        def step():
-            return D.segment_videos_sharded(videos, model, num_clips=fuse, step=args.step,
-                                            fuse_method=args.fuse_method, rank=rank, world=world,
-                                            batch_size=args.batch_size, lengths=lengths)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    evs.clear()
+    dt, kt, out = timed(step, steps, 0, eng, world, dev)
+    ex_ms = sum(a.elapsed_time(b) for a, b in evs) / steps if evs else 0.0
+    t = torch.tensor([ex_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    fwd = forward_stats(kt, (hi - lo) * steps, GFLOP_PER_CLIP, peak, args.dtype)
+    rows, nbytes = D.exchange_stats(lengths, fuse, args.step, world)
+    mine = {"rank": rank, "clips": hi - lo, "videos_held": len(needed), "videos_fused": len(out),
+            "forward_ms_per_step": round(sum(v["ms"] for v in kt.values()) / steps, 3)}
+    per_rank = gather_ranks(mine, world)
+    del videos
+    torch.cuda.empty_cache()
+    return {"value": round(n_total * steps / dt, 3), "unit": "clips/s", "ms_per_step": round(dt / steps * 1e3, 3),
+            "clips_per_step": n_total, "fuse": fuse, "forward": fwd, "per_rank": per_rank,
+            "rows_exchanged_per_step": rows, "bytes_exchanged_per_step": nbytes,
+            "exchange_ms_per_step": round(float(t.item()), 4),
+            "exchange_note": "margin planes (fp32, 32 x 112 x 112 per crossing clip) through one all_to_all_single "
+                             "(RCCL over xGMI with nccl; host-staged with gloo); time = events on the compute stream "
+                             "around logit_margin + the collective, max over ranks (includes waiting for the "
+                             "slowest rank's forward)",
+            "roofline": kernel_roofline(kt, peak, args.dtype), "kt": kt, "out": out}
 
-        dt, kt, out = timed(step, steps, warmup, eng, world, dev)
-        fwd = forward_stats(kt, (hi - lo) * steps, GFLOP_PER_CLIP, peak)
-        rows, nbytes = D.exchange_stats(lengths, fuse, args.step, world)
-        mine = {"rank": rank, "clips": hi - lo, "videos_held": len(needed), "videos_fused": len(out),
-                "forward_ms_per_step": round(sum(v["ms"] for v in kt.values()) / steps, 3)}
-        per_rank = gather_ranks(mine, world)
-        del videos
-        torch.cuda.empty_cache()
-        return {"value": round(n_total * steps / dt, 3), "unit": "clips/s", "ms_per_step": round(dt / steps * 1e3, 3),
-                "clips_per_step": n_total, "fuse": fuse, "forward": fwd, "per_rank": per_rank,
-                "rows_exchanged_per_step": rows, "bytes_exchanged_per_step": nbytes,
-                "roofline": kernel_roofline(kt, peak, args.dtype), "kt": kt, "out": out}
 
-    main_run = one(args.fuse, args.steps, args.warmup)
+def run_c2(args, model, world, rank, dev):
+    """BASELINE config[2]: a fixed batch of full videos (64 x 200 frames, or seeded ragged 100-300-frame
+    lengths with --c2-lengths ragged) sharded clip-wise over the ranks (strong scaling). f = 1: 384
+    clips for the equal batch; the fuse_extra run repeats it with f = 5."""
+    lengths = c2_lengths(args)
+    main_run = c2_measure(args, model, world, rank, dev, lengths, args.fuse, args.steps, args.warmup)
     extra = None
     if args.c2_extra_fuse and args.c2_extra_fuse != args.fuse:
-        extra = one(args.c2_extra_fuse, max(2, args.steps // 3), 1)
+        extra = c2_measure(args, model, world, rank, dev, lengths, args.c2_extra_fuse, max(2, args.steps // 3), 1)
         extra = {k: v for k, v in extra.items() if k not in ("kt", "out")}
     lv = [float(o.float().mean().item()) for o in main_run["out"].values()]
     lv_all = gather_ranks(lv, world)
+    desc = (f"{args.c2_videos} videos x {args.frames} frames" if args.c2_lengths == "equal" else
+            f"{args.c2_videos} videos of seeded EchoNet-like lengths 100-300 frames ({sum(lengths)} frames)")
     return {
         "metric": METRIC, "value": main_run["value"], "unit": "clips/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": main_run["ms_per_step"], "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic EchoNet-style videos (seeded), seeded synthetic weights (" + BENCH_WEIGHTS + " recipe)",
-        "config": {"workload": f"BASELINE config[2]: batch of {args.c2_videos} videos x {args.frames} frames, "
+        "config": {"workload": f"BASELINE config[2]: batch of {desc}, "
                                f"{args.fuse} shifted pass(es), clips sharded over {world} rank(s) + per-frame "
                                f"{args.fuse_method} fusion on each video's owner",
-                   "videos": args.c2_videos, "frames": args.frames, "fuse": args.fuse, "step": args.step,
+                   "videos": args.c2_videos, "frames": args.frames if args.c2_lengths == "equal" else lengths,
+                   "fuse": args.fuse, "step": args.step,
                    "clips_per_step": main_run["clips_per_step"], "batch_size": args.batch_size,
                    "parallelism": f"clip-shard x{world} ({args.dist_backend}); owner all_to_all of logit margins "
                                   f"only for straddling videos"},
         "roofline": main_run["roofline"], "forward": main_run["forward"], "per_rank": main_run["per_rank"],
         "rows_exchanged_per_step": main_run["rows_exchanged_per_step"],
         "bytes_exchanged_per_step": main_run["bytes_exchanged_per_step"],
+        "exchange_ms_per_step": main_run["exchange_ms_per_step"],
         "fuse_extra": extra, "lv_fraction": round(float(np.mean(sum(lv_all, []))), 4),
     }
 
@@ -449,7 +548,7 @@ def run_c1(args, model, world, rank, dev):
     dt, ktimes, out = timed(step, args.steps, args.warmup, eng, world, dev)
     value = n_total * args.steps / dt
     peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else FP32_PEAK_TFLOPS
-    fwd = forward_stats(ktimes, (hi - lo) * args.steps, GFLOP_PER_CLIP, peak)
+    fwd = forward_stats(ktimes, (hi - lo) * args.steps, GFLOP_PER_CLIP, peak, args.dtype)
     lv_frac = float(np.mean([o.float().mean().item() for o in out.values()])) if out else 0.0
     parity = northstar_parity(args, out[0], args.dtype) if 0 in out else None
     parity_random = random_recipe_parity(args, model, step, args.dtype) if world == 1 and args.parity_random else None
@@ -463,15 +562,29 @@ def run_c1(args, model, world, rank, dev):
         d16 = [1.0 - categorical_dice(out16[k].cpu().numpy(), ref_masks[k].cpu().numpy(), 1) for k in out16]
         bf16 = {"value": round(n_total * args.steps / dt16, 3), "unit": "clips/s",
                 "ms_per_step": round(dt16 / args.steps * 1e3, 3),
-                "forward": forward_stats(k16, (hi - lo) * args.steps, GFLOP_PER_CLIP, BF16_PEAK_TFLOPS),
+                "forward": forward_stats(k16, (hi - lo) * args.steps, GFLOP_PER_CLIP, BF16_PEAK_TFLOPS, "bf16"),
                 "dice_delta_vs_fp32_fused_masks": round(float(max(d16)) if d16 else 0.0, 6),
                 "parity_vs_cpu": northstar_parity(args, out16[0], "bf16") if 0 in out16 else None,
+                "parity_vs_cpu_random_weights": (random_recipe_parity(args, model, step, "bf16")
+                                                 if world == 1 and args.parity_random else None),
                 "roofline": kernel_roofline(k16, BF16_PEAK_TFLOPS, "bf16"),
+                "kernels": kernel_table(k16, "bf16"),
                 "note": "BASELINE config[4]: bf16 activations/weights, fp32 accumulate, fp32 decoder head; "
                         "Dice tolerance 1e-2"}
         model.set_compute_dtype("fp32")
 
     c3 = c3_run(args, model, world, dev, max(2, args.steps // 2), 1) if args.extra_c3 else None
+
+    # N > 1: the ragged config[2] batch, whose straddling videos move logit margins between ranks (the
+    # c1 layout, one equal video per rank, exchanges nothing)
+    c2r = None
+    if args.extra_c2_ragged and world > 1:
+        import clasfv_amd.synthetic as S
+        c2r = c2_measure(args, model, world, rank, dev, S.echonet_like_lengths(args.c2_videos), 1,
+                         max(2, args.steps // 2), 1)
+        c2r = {k: v for k, v in c2r.items() if k not in ("kt", "out", "roofline")}
+        c2r["workload"] = (f"BASELINE config[2] with ragged lengths: {args.c2_videos} seeded EchoNet-like videos of "
+                           f"100-300 frames, f = 1, clips sharded over {world} ranks (strong scaling)")
 
     stream = None
     if args.extra_stream and world == 1:
@@ -522,10 +635,7 @@ def run_c1(args, model, world, rank, dev):
                                   f"(owner all_to_all of logit margins only for straddling videos)"},
         "roofline": kernel_roofline(ktimes, peak, args.dtype),
         "forward": fwd,
-        "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
-                        "issued_tflops": round(v["xgflop"] / max(v["ms"], 1e-9), 2),
-                        "algorithmic_tflops": round(v["gflop"] / max(v["ms"], 1e-9), 2)}
-                    for k, v in ktimes.items()},
+        "kernels": kernel_table(ktimes, args.dtype),
         "cpu_baseline": cpu,
         "dice_delta_vs_cpu": parity and parity["dice_delta_fused_masks"],
         "ef_delta_vs_cpu": parity and parity["ef_delta_max_per_systole"],
@@ -533,6 +643,7 @@ def run_c1(args, model, world, rank, dev):
         "parity_random_weights": parity_random,
         "bf16": bf16,
         "config3": c3,
+        "c2_ragged": c2r,
         "stream": stream,
         "lv_fraction": round(lv_frac, 4),
     }

@@ -73,7 +73,9 @@ def load():
         import sys
         print(f"clasfv: {LIB_PATH} {'missing' if have is None and not os.path.exists(LIB_PATH) else 'stale'} "
               f"(library source hash {have}, sources {want}): rebuilding", file=sys.stderr)
-        B.build(force=B.library_hash() != want)
+        # not forced: build() re-checks the hash under its lock, so ranks that waited for another
+        # rank's rebuild reuse it instead of compiling again
+        B.build()
         if B.library_hash() != want:
             raise RuntimeError(f"{LIB_PATH}: rebuild did not produce a library of the current sources")
     lib = ctypes.CDLL(LIB_PATH)

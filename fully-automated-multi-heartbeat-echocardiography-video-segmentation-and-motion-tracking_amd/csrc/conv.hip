@@ -1001,8 +1001,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 
 // conv_proj_x3: fp32 1x1x1 stride-1 convs to 64 channels over K = Cin (+ Cin2) = 128, both inputs
 // multiples of 32 channels, channels-last in and out, no split-K (the decoder projections P01 and P2;
-// K = 256 (P3) needs more registers than the item ring leaves and stays on conv_dma_x3)
+// K = 256 (P3) needs more registers than the item ring leaves and stays on conv_dma_x3). A split-bf16
+// kernel: the no_dma_x3 variant (every non-stem GEMM on f32 MFMAs) excludes it too.
 bool proj_x3_supported(const ConvParams& p) {
+  if (p.vflags & CLASFV_VARIANT_NO_DMA_X3) return false;
   if (p.in_bf16 || p.out_bf16 || p.stem || p.x_c8 || p.y_c8 || p.n_split > 1) return false;
   if (p.KT != 1 || p.KH != 1 || p.KW != 1 || p.st != 1 || p.sh != 1 || p.sw != 1) return false;
   if (p.Cout != 64 || p.Cin % 32 || (p.x2 && p.Cin2 % 32)) return false;

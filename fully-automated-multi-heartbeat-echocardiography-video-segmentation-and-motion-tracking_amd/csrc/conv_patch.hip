@@ -740,11 +740,14 @@ hipError_t launch_p32(const ConvParams& p, hipStream_t s) {
 // (convbench, profiles/r04_patch32_bf16.txt: layer1 0.686 vs 0.726 ms, layer2 288 channels at NB 3
 // 0.325 vs 0.313, layer3 576 at NB 3 0.152 vs 0.156, layer4 1152 at NB 2 0.114 vs 0.088). 0: not
 // taken. force_nb > 0 (convbench, CLASFV_PATCH_NT = -NB) takes any NB that divides.
+// The size rule counts blocks PER CLIP (>= 128: every 112x112-clip layer1 map; 32x112x112 gives 392),
+// never the batch's, so whether a clip's layer1 runs 32x32x16 or 16x16x32 products -- and so its
+// rounding -- does not depend on how many clips share the launch.
 int patch32_pick_nb(const ConvParams& p, int force_nb) {
   if (p.Cout % 32) return 0;
   const int n32 = p.Cout / 32;
   if (force_nb > 0) return (force_nb <= 5 && force_nb >= 2 && n32 % force_nb == 0) ? force_nb : 0;
-  return n32 % 5 == 0 && patch_grid(p, 4).base * (n32 / 5) >= 512 ? 5 : 0;
+  return n32 % 5 == 0 && patch_grid(p, 4).base / p.N * (n32 / 5) >= 128 ? 5 : 0;
 }
 
 }  // namespace

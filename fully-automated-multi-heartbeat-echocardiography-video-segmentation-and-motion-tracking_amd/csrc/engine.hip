@@ -354,8 +354,12 @@ double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
   if (!strcmp(kname, "conv_wino_q") || !strcmp(kname, "conv_wino"))
     return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 1) / 2) * 16.0 * cc * 1e-9;
   if (!strcmp(kname, "conv_winot")) return 2.0 * out.n * (out.t / 4) * (double)out.h * out.w * 6.0 * cc * 1e-9;
-  if (!strcmp(kname, "conv_stem_x3"))  // the fp32 GEMM it computes (K = 7 rows x 8 taps x 4 channels)
-    return 2.0 * ceil((double)out.n * out.t * out.h * out.w / 256.0) * 256.0 * 48.0 * 224.0 * 1e-9;
+  // Split-bf16 ("x3") kernels of the fp32 engines run on the bf16 matrix pipe: their work is counted
+  // in that pipe's own products, six bf16 products per product of the fp32 GEMM they compute (the
+  // f32-MFMA kernels count f32 products), so each kernel's rate compares with the peak of the pipe it
+  // issues to (bench.py rates them against 2.5 PFLOP/s, the f32 ones against 157.3 TFLOP/s).
+  if (!strcmp(kname, "conv_stem_x3"))  // 6 x the fp32 GEMM (K = 7 rows x 8 taps x 4 channels)
+    return 6 * 2.0 * ceil((double)out.n * out.t * out.h * out.w / 256.0) * 256.0 * 48.0 * 224.0 * 1e-9;
   if (!strcmp(kname, "conv_stem_bf16"))
     return 3 * 2.0 * ceil((double)out.n * out.t * out.h * out.w / 256.0) * 256.0 * 64.0 * 224.0 * 1e-9;
   if (!strcmp(kname, "conv_patch_bf16")) {  // frames x 64-pixel tiles: 2 x 8x8 for 1x3x3, 4 x 64 flat for 3x1x1
@@ -364,16 +368,15 @@ double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
                                 : (double)((out.h * out.w + 63) / 64 * 64);
     return 2.0 * out.n * ((out.t + fr - 1) / fr * fr) * px * c.cout_p * (double)c.Kp * 1e-9;
   }
-  if (!strcmp(kname, "conv_proj_x3"))  // 32-voxel items, the fp32 GEMM it computes
-    return 2.0 * ceil((double)out.n * out.t * out.h * out.w / 32.0) * 32.0 * c.cout_p * (double)c.Kp * 1e-9;
+  if (!strcmp(kname, "conv_proj_x3"))  // 32-voxel items, 6 x the fp32 GEMM it computes
+    return 6 * 2.0 * ceil((double)out.n * out.t * out.h * out.w / 32.0) * 32.0 * c.cout_p * (double)c.Kp * 1e-9;
   if (!strcmp(kname, "conv_patch32_bf16"))  // 4 frames x 8x8-pixel tiles
     return 2.0 * out.n * ((out.t + 3) / 4 * 4) * (double)((out.h + 7) / 8 * 8) * ((out.w + 7) / 8 * 8) * c.cout_p *
            (double)c.Kp * 1e-9;
   const double m = (double)out.n * out.t * out.h * out.w;
-  // conv_dma_x3: the fp32 GEMM it computes (K padded to 32-deep pairs), priced like the fp32 MFMA
-  // kernels; its six bf16 products per K block run on the bf16 matrix rate
+  // conv_dma_x3: six bf16 products per product of the fp32 GEMM it computes (K padded to 32-deep pairs)
   if (!strcmp(kname, "conv_dma_x3"))
-    return 2.0 * (ceil(m / 128.0) * 128.0) * c.cout_p * (double)((c.Kp + 31) / 32 * 32) * 1e-9;
+    return 6 * 2.0 * (ceil(m / 128.0) * 128.0) * c.cout_p * (double)((c.Kp + 31) / 32 * 32) * 1e-9;
   return 2.0 * (ceil(m / 128.0) * 128.0) * c.cout_p * (double)c.Kp * 1e-9;
 }
 
@@ -1043,10 +1046,13 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   d.w2x3 = h->w2x3;
   d.x3 = h->dtype != CLASFV_DTYPE_BF16 && !(h->tune.vflags & CLASFV_VARIANT_NO_DECODER_X3);
   HIP_TRY(launch_decoder(d, s));
-  // comb_2 (64x64; three split-bf16 products in bf16 engines, six in fp32 ones) and the heads (6
-  // useful of the 16 rows of their MFMA tile) per output voxel
-  timed("decoder_kernel", 2.0 * N * (double)T * H * W * (64 * 64 + 64 * 6) * 1e-9,
-        2.0 * N * (double)T * H * W * ((d.bf16 ? 3 : 1) * 64 * 64 + 64 * 16) * 1e-9);
+  // comb_2 (64x64) and the heads (6 useful of the 16 rows of their MFMA tile) per output voxel, in the
+  // products of the pipe they run on: fp32 engines six split-bf16 products each (bf16 pipe), bf16
+  // engines three for comb_2 and six for the heads (bf16 pipe), the no_decoder_x3 variant one f32
+  // product each (f32 pipe)
+  const double dec_px = d.x3 ? 6.0 * (64 * 64 + 64 * 16) : d.bf16 ? 3.0 * 64 * 64 + 6.0 * 64 * 16 : 64 * 64 + 64 * 16;
+  timed(d.x3 || d.bf16 ? "decoder_kernel" : "decoder_kernel_f32", 2.0 * N * (double)T * H * W * (64 * 64 + 64 * 6) * 1e-9,
+        2.0 * N * (double)T * H * W * dec_px * 1e-9);
   return CLASFV_OK;
 }
 

@@ -132,10 +132,14 @@ def exchange_to_owners(local, owners, rank, world, group=None, force=False):
     send = local[torch.tensor([g - lo for g in order], dtype=torch.long, device=local.device)] if order else local
     send_sizes = counts[rank]
     recv_sizes = [counts[s_][rank] for s_ in range(world)]
-    out = torch.empty((sum(recv_sizes),) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    dist.all_to_all_single(out, send.contiguous(), output_split_sizes=recv_sizes, input_split_sizes=send_sizes,
+    # gloo (the CPU / several-ranks-on-one-GPU rehearsal of the RCCL path) exchanges host tensors
+    stage = local.is_cuda and dist.get_backend(group) == "gloo"
+    dev = "cpu" if stage else local.device
+    out = torch.empty((sum(recv_sizes),) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+    dist.all_to_all_single(out, send.contiguous().to(dev), output_split_sizes=recv_sizes, input_split_sizes=send_sizes,
                            group=group)
-    return out  # source blocks are in rank order and each is in global order: global order overall
+    # source blocks are in rank order and each is in global order: global order overall
+    return out.to(local.device) if stage else out
 
 
 def videos_needed(lengths, num_clips, step, rank, world, interpolate_last=True):
@@ -155,14 +159,17 @@ def exchange_stats(lengths, num_clips, step, world, h=112, w=112, interpolate_la
 
 
 def segment_videos_sharded(videos_dev, model, num_clips=5, step=1, fuse_method="simple", interpolate_last=True,
-                           rank=0, world=1, batch_size=None, clip_fn=None, lengths=None, force_exchange=False):
+                           rank=0, world=1, batch_size=None, clip_fn=None, lengths=None, force_exchange=False,
+                           exchange_events=None):
     """Fuse a batch of device videos (each (3,T,H,W)) with clips sharded over ranks.
 
     Returns {video index: fused (T',H,W) uint8 device tensor} for the videos this rank owns
     (video_owners). ``clip_fn(clips) -> logits`` overrides the model call. With ``lengths`` (the
     frame count of every video) ``videos_dev`` may hold None for videos outside this rank's block
     (``videos_needed``). ``force_exchange``: ship logit margins through the all_to_all even when no
-    clip crosses ranks (tests; the result is the same)."""
+    clip crosses ranks (tests; the result is the same). ``exchange_events``: a list that receives one
+    (start, end) pair of timing events on the current stream around the margin computation and the
+    all_to_all, when the exchange runs (bench.py reports their elapsed time)."""
     if lengths is None:
         lengths = [v.shape[1] for v in videos_dev]
     plans, n_total = global_clip_plan(list(lengths), num_clips, step, interpolate_last)
@@ -189,9 +196,16 @@ def segment_videos_sharded(videos_dev, model, num_clips=5, step=1, fuse_method="
     local = compute(lo, hi) if hi > lo else empty
     owners = owner_of_clips(plans, world)
     margin = force_exchange or (world > 1 and rows_exchanged(owners, world) > 0)
+    ev = None
+    if margin and exchange_events is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     if margin:  # ship one fp32 plane per clip frame instead of two (bit-identical labels, see above)
         local = FU.logit_margin(local) if local.shape[0] else local[:, 0]
     mine = exchange_to_owners(local.contiguous(), owners, rank, world, force=force_exchange)
+    if ev is not None:
+        ev[1].record()
+        exchange_events.append(ev)
     vown = video_owners(plans, world)
     out, at = {}, 0
     for vi, p in enumerate(plans):

@@ -44,3 +44,11 @@ def echo_video_uint8(T=200, H=112, W=112, seed=0, period=50):
 def echo_video(T=200, H=112, W=112, seed=0, period=50):
     """(3,T,H,W) float32 video after the CLI's transpose (motion_segment.py:96), not normalised."""
     return np.ascontiguousarray(echo_video_uint8(T, H, W, seed, period).transpose(3, 0, 1, 2), dtype=np.float32)
+
+
+def echonet_like_lengths(n, seed=2024, lo=100, hi=300):
+    """Seeded ragged video lengths in [lo, hi] frames (EchoNet-Dynamic clips run ~100-300 frames at
+    50 fps): the config[2] batch with lengths that make videos straddle the ranks' clip blocks, so the
+    owner exchange (dist.exchange_to_owners) moves logit margins over RCCL."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return [int(t) for t in rng.integers(lo, hi + 1, size=n)]

@@ -4,8 +4,9 @@ Tolerances: the forward is fp32 with a different summation order than cuDNN/mkld
 implicit GEMMs, folded BatchNorm, decoder commuted to project-then-interpolate), so raw logits are
 compared with an absolute tolerance and the derived masks with the north_star bar Dice delta <= 1e-3.
 The logit tolerance sits a few times above the largest error measured on the box over every shape
-tested here (profiles/r03a_parity_errors.txt: seg <= 2.1e-5 at config[3] 64x224x224, <= 1.6e-5 at
-32x112x112; motion <= 5.5e-7), so a kernel bug that moves one channel block by 1e-4 fails.
+tested here (profiles/r04pe_parity_errors.txt, on the round-4 kernels: seg <= 2.6e-5 at config[3]
+64x224x224, <= 1.8e-5 at 32x112x112; motion <= 5.9e-7), so a kernel bug that moves one channel block
+by 1e-4 fails.
 Plumbing kernels (clip building, resample, argmax, voting, normaliser) are compared bit for bit.
 """
 import os
@@ -21,8 +22,8 @@ from tests.golden.fake_model import fake_model
 pytestmark = pytest.mark.gpu
 
 DICE_TOL = 1e-3
-SEG_ATOL = 1e-4   # fp32 logits (measured max 2.1e-5)
-MOT_ATOL = 2e-6   # fp32 tanh motion (measured max 5.5e-7)
+SEG_ATOL = 1e-4   # fp32 logits (measured max 2.6e-5, r04pe)
+MOT_ATOL = 2e-6   # fp32 tanh motion (measured max 5.9e-7, r04pe)
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -108,6 +109,28 @@ def test_forward_batch_is_per_clip_exact_ragged_tiles(model, shape):
     for i in range(shape[0]):
         s1, m1 = model(x[i:i + 1])
         assert torch.equal(s1[0], seg[i]) and torch.equal(m1[0], mot[i]), i
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 32, 112, 112), (3, 3, 24, 80, 112)])
+def test_bf16_forward_batch_is_per_clip_exact(shape):
+    """config[4] engines: every kernel choice is a per-clip shape rule too (conv_patch32_bf16 is taken
+    from the per-clip block count, not the batch's), so one clip alone and the same clip inside a
+    batch get the same products in the same order -- bit-identical, with the 32x32x16 kernel running
+    at N = 1 as well."""
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    rng = np.random.default_rng(sum(shape) + 1)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    m16 = R2plus1D_18_MotionNet(pretrained=False, dtype="bf16")
+    seg, mot = m16(x)
+    m16.engine.set_kernel_timing(True)
+    s1, m1 = m16(x[:1])
+    kt = m16.engine.kernel_timing(cap=32)
+    m16.engine.set_kernel_timing(False)
+    assert "conv_patch32_bf16" in kt
+    assert torch.equal(s1[0], seg[0]) and torch.equal(m1[0], mot[0])
+    for i in range(1, shape[0]):
+        si, mi = m16(x[i:i + 1])
+        assert torch.equal(si[0], seg[i]) and torch.equal(mi[0], mot[i]), i
 
 
 def test_forward_rejects_bad_shapes(model):
@@ -682,8 +705,14 @@ def test_x3_convs_match_fp32_mfma(model, shape, variant):
     x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
     s3, m3 = model(x)
     model.set_kernel_variants(variant)
+    model.engine.set_kernel_timing(True)
     s1, m1 = model(x)
+    kt = model.engine.kernel_timing(cap=32)
+    model.engine.set_kernel_timing(False)
     model.set_kernel_variants()
+    # the variant really moves those GEMMs (the decoder projections included) onto f32 MFMAs
+    gone = ("conv_dma_x3", "conv_proj_x3") if variant == "no_dma_x3" else ("conv_stem_x3",)
+    assert not any(k in kt for k in gone), sorted(kt)
     assert not torch.equal(s3, s1)  # the split-bf16 GEMM really ran
     np.testing.assert_allclose(s3.cpu().numpy(), s1.cpu().numpy(), rtol=0, atol=SEG_ATOL)
     np.testing.assert_allclose(m3.cpu().numpy(), m1.cpu().numpy(), rtol=0, atol=MOT_ATOL)
@@ -755,8 +784,11 @@ def test_northstar_config1_fused_masks_and_ef_vs_cpu(request, recipe, method):
     """north_star bar (BASELINE.json): fused masks Dice delta <= 1e-3 and EF within 1e-3 of the CPU
     reference path, on config[1] with the real HIP model, through the drop-in
     segment_a_video_with_fusion (src/fuse_utils.py:36-100) and compute_ef_using_putative_clips
-    (src/fuse_utils.py:105-148), for both weight recipes. SIMPLE / STAPLE fusion: the CPU side is the
-    oracle restatement (LabelFusion absent: parity with LabelFusion itself unpinned)."""
+    (src/fuse_utils.py:105-148), for both weight recipes. The EF bar is 1e-3 for the echo recipe
+    (physiological EFs); the random recipe's EFs sit near 100 % (ES volume ~0), where one pixel moves
+    the EF by ~1e-3, so its EF bar is 1e-2 and that recipe is judged by Dice delta <= 1e-3 and
+    identical ED/ES pairs. SIMPLE / STAPLE fusion: the CPU side is the oracle restatement
+    (LabelFusion absent: parity with LabelFusion itself unpinned)."""
     from clasfv_amd import fuse_utils as FU
     from clasfv_amd.echo import compute_ef_using_putative_clips
     model = _recipe_model(request, recipe)
@@ -894,14 +926,17 @@ def test_video_stream_matches_per_video_pipeline(model):
 
 # ---- round 3: config[4] on the north_star video, CLI vs the CPU path, non-strict plumbing -------
 
-def test_northstar_config4_bf16_fused_masks_vs_cpu():
+@pytest.mark.parametrize("recipe", ["echo", "random"])
+def test_northstar_config4_bf16_fused_masks_vs_cpu(recipe):
     """BASELINE config[4] bar on the config[1] video: the bf16 engine's fused masks (SIMPLE, 5 passes)
-    against the CPU reference path's fp32 masks: Dice delta <= 1e-2, same ED/ES pairs, EF close."""
+    against the CPU reference path's fp32 masks: Dice delta <= 1e-2, same ED/ES pairs, EF close. Both
+    weight recipes: with the echo weights layer2-4 reach the LV margin at ~1e-2 only, so the random
+    recipe (every layer at full gain) is the case where bf16 rounding in layer2-4 can move masks."""
     from clasfv_amd import fuse_utils as FU
     from clasfv_amd.echo import compute_ef_using_putative_clips
     from clasfv_amd.model import R2plus1D_18_MotionNet
-    g, video = _northstar()
-    m16 = R2plus1D_18_MotionNet(pretrained=False, weights="echo", dtype="bf16")
+    g, video = _northstar(recipe)
+    m16 = R2plus1D_18_MotionNet(pretrained=False, weights=recipe, dtype="bf16")
     out = FU.segment_a_video_with_fusion(video, m16, num_clips=int(g["fuse"]), step=int(g["step"]),
                                          fuse_method="simple")
     shp = tuple(g["fused_simple_shape"])
@@ -1119,8 +1154,74 @@ def test_config2_64_videos_over_8_ranks_equals_one_rank(echo_model):
         assert got[v] == hashlib.sha1(ref[v].cpu().numpy().tobytes()).hexdigest(), v
 
 
+def _c2r_worker(rank, world, port, q, lengths):
+    import hashlib
+    import os
+    import torch.distributed as dist
+    import clasfv_amd.synthetic as S
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from clasfv_amd import dist as D
+        from clasfv_amd.model import R2plus1D_18_MotionNet
+        from clasfv_amd.preprocess import zeroone_normalize_
+        m = R2plus1D_18_MotionNet(pretrained=False, weights="echo")
+        need = D.videos_needed(lengths, 1, 1, rank, world)
+        vids = [None] * len(lengths)
+        for v in need:
+            vids[v] = zeroone_normalize_(torch.from_numpy(S.echo_video(lengths[v], seed=v)).cuda())
+        evs = []
+        out = D.segment_videos_sharded(vids, m, num_clips=1, step=1, fuse_method="simple", rank=rank, world=world,
+                                       lengths=lengths, exchange_events=evs)
+        torch.cuda.synchronize()
+        q.put((rank, len(evs), {k: hashlib.sha1(v.cpu().numpy().tobytes()).hexdigest() for k, v in out.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_config2_ragged_over_8_ranks_exchanges_and_equals_one_rank(echo_model):
+    """config[2] with ragged EchoNet-like lengths (16 seeded videos of 100-300 frames, f = 1) over 8
+    ranks (gloo, all on the box's one GPU): videos straddle the clip blocks, so the owner all_to_all
+    really moves logit margins (rows_exchanged > 0, every rank records the exchange), and every fused
+    mask is bit-identical to the 1-rank result."""
+    import hashlib
+    import socket
+    import torch.multiprocessing as mp
+    import clasfv_amd.synthetic as S
+    from clasfv_amd import dist as D
+    from clasfv_amd.preprocess import zeroone_normalize_
+    world = 8
+    lengths = S.echonet_like_lengths(16, seed=7)
+    rows, nbytes = D.exchange_stats(lengths, 1, 1, world)
+    assert rows > 0 and nbytes == rows * 32 * 112 * 112 * 4
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_c2r_worker, args=(r, world, port, q, lengths)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, n_ev, out = q.get(timeout=600)
+        assert n_ev == 1, (r, n_ev)
+        assert not set(out) & set(got)
+        got.update(out)
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert sorted(got) == list(range(len(lengths)))
+    vids = [zeroone_normalize_(torch.from_numpy(S.echo_video(t, seed=v)).cuda()) for v, t in enumerate(lengths)]
+    ref = D.segment_videos_sharded(vids, echo_model, num_clips=1, step=1, fuse_method="simple")
+    for v in range(len(lengths)):
+        assert got[v] == hashlib.sha1(ref[v].cpu().numpy().tobytes()).hexdigest(), v
+
+
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("workload", ["c1", "c2"])
+@pytest.mark.parametrize("workload", ["c1", "c2", "c2r"])
 def test_bench_self_launches_ranks(workload):
     """`bench.py --gpus 2` without a launcher starts the 2 rank processes itself (here over gloo, both
     on the one GPU) and rank 0 prints one JSON line with n_gpus == 2; under a launcher WORLD_SIZE must
@@ -1130,9 +1231,13 @@ def test_bench_self_launches_ranks(workload):
     import sys
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--steps", "2", "--warmup", "1",
            "--extra-bf16", "0", "--extra-c3", "0", "--extra-stream", "0", "--cpu-baseline", "0",
-           "--workload", workload]
+           "--workload", workload[:2]]
     if workload == "c2":
         cmd += ["--c2-videos", "8", "--c2-extra-fuse", "0"]
+    if workload == "c2r":  # ragged lengths: the owner exchange runs and is timed
+        cmd += ["--c2-videos", "8", "--c2-extra-fuse", "0", "--c2-lengths", "ragged"]
+    if workload == "c1":  # the c1 line's ragged config[2] extra, kept small here
+        cmd += ["--c2-videos", "8"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=REPO, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -1141,8 +1246,14 @@ def test_bench_self_launches_ranks(workload):
     if workload == "c2":
         assert line["scaling"] == "strong" and line["rows_exchanged_per_step"] == 0
         assert [p["clips"] for p in line["per_rank"]] == [24, 24]
+    elif workload == "c2r":
+        assert line["scaling"] == "strong" and line["rows_exchanged_per_step"] > 0
+        assert line["bytes_exchanged_per_step"] == line["rows_exchanged_per_step"] * 32 * 112 * 112 * 4
+        assert line["exchange_ms_per_step"] > 0
     else:
         assert line["config"]["clips_per_step"] == 60
+        c2r = line["c2_ragged"]
+        assert c2r["rows_exchanged_per_step"] > 0 and c2r["exchange_ms_per_step"] > 0
 
 
 # ---- round 4: RCCL on the leased GPU, config[0] through the CLI ------------------------------------

@@ -278,6 +278,34 @@ def test_fast_division_magic_numbers(tmp_path):
     assert "(((1ull << 32) * ((1ull << l) - d)) / d + 1)" in hdr  # the construction the check restates
 
 
+def test_wino4w_inline_asm_accumulators_untouched(tmp_path):
+    """conv_wino4w's N tiles past W4W_NTA accumulate in VGPRs through inline-asm MFMAs that hipcc
+    neither models nor pads: the product build is safe only while no compiler instruction in the
+    chunk loop (or between the loop exit and the 12-state drain) touches those registers and the
+    kernel has no scratch. tools/audit_wino4w_asm.py checks that on the device assembly of every
+    conv_wino4w instantiation (and flags an injected v_mov into an accumulator)."""
+    import shutil
+    import sys
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    if not os.path.exists(hipcc) and shutil.which("hipcc") is None:
+        pytest.skip("hipcc not available")
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import audit_wino4w_asm as A
+    path = A.compile_asm(out_dir=str(tmp_path))
+    problems, n = A.audit(path)
+    assert n >= 8 and problems == [], problems
+    # the audit sees a violation: a compiler copy into the first asm accumulator inside the loop
+    lines = open(path).read().splitlines()
+    k = next(i for i, ln in enumerate(lines) if "v_mfma_f32_16x16x4_f32 v[" in ln)
+    acc = int(re.search(r"v\[(\d+):", lines[k]).group(1))
+    j = next(i for i in range(k, 0, -1) if ";;#ASMSTART" in lines[i])
+    lines.insert(j, f"\tv_mov_b32 v{acc}, 0")
+    bad = tmp_path / "bad.s"
+    bad.write_text("\n".join(lines))
+    problems, _ = A.audit(str(bad))
+    assert len(problems) == 1 and f"v{acc}" in problems[0]
+
+
 def test_strict_reference_clamp_and_frames():
     """src/fuse_utils.py:38-42 clamps T in [32, 32 + step) to K = 0 (then IndexError at :82);
     strict_reference=False runs one pass there, and keeps all T frames for step > 1 (:85)."""
