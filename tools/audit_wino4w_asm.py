@@ -94,17 +94,24 @@ def audit_function(name, body):
         if re.match(r"^\.LBB\w+:", ln):
             label = ln
         in_loop[k] = label is not None and "Loop" in label
-    # the loop exit prefix: from the first non-loop label after the loop to the drain statement
-    last_loop = max(k for k in range(len(body)) if in_loop[k])
-    drain = None
-    for k in range(last_loop + 1, len(body)):
-        if in_asm[k] and "s_nop 7" in body[k]:
-            drain = k
-            break
-    if drain is None:
-        problems.append(f"{name}: no w4w_drain nop statement after the chunk loop")
-        drain = last_loop + 1
-    check = [k for k in range(len(body)) if (in_loop[k] or last_loop < k < drain) and not in_asm[k]]
+    # each chunk loop (a run of loop blocks; the two-item form has two) and its exit prefix: from the
+    # loop's last line to the next drain statement
+    exits = set()
+    k = 0
+    while k < len(body):
+        if in_loop[k]:
+            e = k
+            while e + 1 < len(body) and in_loop[e + 1]:
+                e += 1
+            drain = next((d for d in range(e + 1, len(body)) if in_asm[d] and "s_nop 7" in body[d]), None)
+            if drain is None:
+                problems.append(f"{name}: no w4w_drain nop statement after the chunk loop ending at line {e}")
+                drain = e + 1
+            exits.update(range(e + 1, drain))
+            k = e + 1
+        else:
+            k += 1
+    check = [k for k in range(len(body)) if (in_loop[k] or k in exits) and not in_asm[k]]
     for k in check:
         s = body[k].split(";")[0].strip()
         if not s or s.endswith(":") or s.startswith("."):
