@@ -81,30 +81,66 @@ __device__ inline void store_out4(void* y, size_t o, f32x4 v, int bf16) {
 // reads its residual vector before writing the same addresses (res may alias y).
 // EF >= 0: the flags at compile time (bit 0 residual, 1 ReLU, 2 8-channel-blocked output; fp32 out),
 // so only one form of each statement is in the code; EF < 0: read from p.
+// Load order: every bias vector (and, where MT x NT <= 16, every residual vector) before the first
+// store, then ONE explicit vmcnt(0). A load issued after a store is waited for with every older
+// vector-memory op (vmcnt retires in order), and the compiler's own waits in the per-element
+// branches were vmcnt(0): the per-element form paid the store latency once per (row, N tile) --
+// MT x NT times per block. Bigger residual tiles load one row at a time (one wait per row).
 template <int MT, int NT, int EF = -1>
 __device__ inline void epilogue(const ConvParams& p, const f32x4 (&acc)[MT][NT], int m_base, int n0, int q, int l16) {
   const bool has_res = EF < 0 ? p.res != nullptr : (EF & 1) != 0;
   const bool relu = EF < 0 ? p.relu != 0 : (EF & 2) != 0;
   const bool c8 = EF < 0 ? p.y_c8 != 0 : (EF & 4) != 0;
   const int obf = EF < 0 ? p.out_bf16 : 0;
+  constexpr bool ALL_ROWS = MT * NT <= 16;
+  f32x4 bv[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int n = n0 + j * 16 + 4 * q;
+    bv[j] = p.bias && n < p.Cout ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // channels-last, or 8-channel blocks [Cout/8][M][8] (p.y_c8, fp32)
+  auto off = [&](int m, int n) { return c8 ? ((size_t)(n >> 3) * p.M + m) * 8 + (n & 7) : (size_t)m * p.Cout + n; };
+  auto load_row = [&](int i, f32x4 (&r)[NT]) __attribute__((always_inline)) {
+    const int m = m_base + i * 16 + l16;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = n0 + j * 16 + 4 * q;
+      r[j] = m < p.M && n < p.Cout ? load_res4(p.res, off(m, n), obf) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  f32x4 rv[ALL_ROWS ? MT : 1][NT];
+  if constexpr (ALL_ROWS) {
+    if (has_res) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) load_row(i, rv[i]);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the epilogue's loads landed (no store issued yet)
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
     const int m = m_base + i * 16 + l16;
+    f32x4 rr[NT];
+    if (has_res) {
+      if constexpr (ALL_ROWS) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) rr[j] = rv[i][j];
+      } else {
+        load_row(i, rr);
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+      }
+    }
     if (m >= p.M) continue;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int n = n0 + j * 16 + 4 * q;
       if (n >= p.Cout) continue;
-      // channels-last, or 8-channel blocks [Cout/8][M][8] (p.y_c8, fp32)
-      const size_t o = c8 ? ((size_t)(n >> 3) * p.M + m) * 8 + (n & 7) : (size_t)m * p.Cout + n;
-      const f32x4 bv = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 rv = has_res ? load_res4(p.res, o, obf) : f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 v = acc[i][j] + bv + rv;
+      f32x4 v = acc[i][j] + bv[j] + (has_res ? rr[j] : f32x4{0.f, 0.f, 0.f, 0.f});
       if (relu) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = relu1(v[c]);
       }
-      store_out4(p.y, o, v, obf);
+      store_out4(p.y, off(m, n), v, obf);
     }
   }
 }

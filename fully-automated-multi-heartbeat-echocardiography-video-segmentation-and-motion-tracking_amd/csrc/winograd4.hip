@@ -266,6 +266,13 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
   const int uR = R0 + useg, uf = fdiv(uR, g.fd_th), uty = uR - uf * g.TH;
   const int uxx = 4 * (tx0 + utc) + ub;
   const bool ulive = utile < NT && uxx < W;
+  // the 3 N tiles' bias vectors before the first store, one explicit vmcnt(0): a bias load after a
+  // store waits for it (vmcnt retires in order), once per N tile in the per-tile form
+  f32x4 biasv[3];
+#pragma unroll
+  for (int nt = 0; nt < 3; ++nt)
+    biasv[nt] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + cob * 48 + nt * 16 + 4 * ucq) : f32x4{0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
   for (int nt = 0; nt < 3; ++nt) {
     __syncthreads();  // the ring (nt = 0) / the previous pass's planes are no longer read
@@ -343,7 +350,7 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2
         }
       }
       const int co = cob * 48 + nt * 16 + 4 * ucq;
-      const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 bias = biasv[nt];
       const f32x4 s12 = P[1] + P[2], d12 = P[1] - P[2], s34 = P[3] + P[4], d34 = P[3] - P[4];
       f32x4 y[4];
       y[0] = P[0] + s12 + s34;

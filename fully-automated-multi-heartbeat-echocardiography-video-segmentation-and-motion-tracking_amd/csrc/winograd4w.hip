@@ -54,6 +54,14 @@ __device__ inline void mfma_v(f32x4& c, float a, float b) {
 }
 __device__ inline void w4w_drain() { asm volatile("s_nop 7\n\ts_nop 4" ::: "memory"); }
 
+#ifdef CLASFV_KNOCKOUTS
+// KO & 512 (tools/convbench diagnostic, not product): per block s_memrealtime (100 MHz) at entry, after
+// the first chunk barrier, after the chunk loop and after the epilogue's stores completed, and the
+// block's HW_ID / XCC_ID (profiles/r05c_wino4w_stamps.txt)
+constexpr int W4W_NSTAMP = 16384;
+__device__ unsigned long long g_w4w_stamps[W4W_NSTAMP][10];
+#endif
+
 template <int DPW>
 constexpr int w4w_lds() {
   return W4Ring<DPW>::LDS > 2 * W4W_ZBUF * 4 ? W4Ring<DPW>::LDS : 2 * W4W_ZBUF * 4;
@@ -62,7 +70,7 @@ constexpr int w4w_lds() {
 // C8: 8-channel-blocked output. DPW: DMA instructions per wave per chunk (W4Ring). KO: timing
 // knock-outs for tools/convbench (0 in the product; results are wrong otherwise): 1 no transform,
 // 2 no U loads in the loop, 4 no epilogue, 8 no DMAs in the loop, 128 the epilogue without its output
-// stores, 256 the serial (unpipelined) epilogue order.
+// stores, 256 the serial (unpipelined) epilogue order, 512 per-block phase stamps (diagnostic builds).
 template <int NTN, bool C8, int DPW, int KO = 0, bool RELU = true>
 __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv_wino4w(ConvParams p,
                                                                                                       W4Geo g) {
@@ -72,6 +80,10 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
   __shared__ __align__(16) char smem[w4w_lds<DPW>()];
   char* sink = smem + NR * STAGE;
 
+#ifdef CLASFV_KNOCKOUTS
+  unsigned long long st_[4] = {0, 0, 0, 0};
+  if constexpr ((KO & 512) != 0) st_[0] = __builtin_amdgcn_s_memrealtime();
+#endif
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(p.x), (short)0, (int)((size_t)p.N * p.Ti * p.Hi * p.Wi * p.Cin * 4), 0x00020000);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -205,6 +217,10 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+#ifdef CLASFV_KNOCKOUTS
+      if constexpr ((KO & 512) != 0)
+        if (k == 0) st_[1] = __builtin_amdgcn_s_memrealtime();
+#endif
       if constexpr ((KO & 8) == 0) {
 #pragma unroll
         for (int d = 2; d < NR; ++d) issue_raw(k + d, (ph + d) % NR);
@@ -248,6 +264,9 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
   if constexpr (NTN > W4W_NTA) w4w_drain();
   __builtin_amdgcn_s_waitcnt(vm_wait(0));  // past-the-end DMAs and U loads drained before LDS is reused
   __syncthreads();
+#ifdef CLASFV_KNOCKOUTS
+  if constexpr ((KO & 512) != 0) st_[2] = __builtin_amdgcn_s_memrealtime();
+#endif
 
   if constexpr ((KO & 4) != 0) {
     float sum = 0.f;
@@ -317,9 +336,16 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
     ybase[aa] = yout + (C8 ? (size_t)(co0 >> 3) * plane + px * 8 + (co0 & 7) : px * CO + co0);
   }
   const size_t nt_step = C8 ? 2 * plane : 16;  // co + 16 per N tile
+  // every N tile's bias, loaded before the first store: a bias load issued between the stores is the
+  // wave's youngest vector-memory op, and its s_waitcnt vmcnt(0) waits for every store issued before
+  // it (vmcnt retires in order) -- the epilogue then paid the store latency once per N tile
+  // (profiles/r05d_wino4w_bias_preload.txt: epilogue 8.56 -> 7.85 us per layer1 block)
+  f32x4 biasv[NTN];
+#pragma unroll
+  for (int nt = 0; nt < NTN; ++nt)
+    biasv[nt] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co0 + nt * 16) : f32x4{0.f, 0.f, 0.f, 0.f};
   auto store_unit = [&](int nt, const f32x4 (&P)[6]) __attribute__((always_inline)) {
-    const int co = co0 + nt * 16;
-    const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 bias = biasv[nt];
     const f32x4 s12 = P[1] + P[2], d12 = psub4(P[1], P[2]), s34 = P[3] + P[4], d34 = psub4(P[3], P[4]);
     f32x4 y[4];
     y[0] = P[0] + s12 + s34;
@@ -370,6 +396,19 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
       if (ulive) store_unit(nt, P);
     }
   }
+#ifdef CLASFV_KNOCKOUTS
+  if constexpr ((KO & 512) != 0) {
+    __builtin_amdgcn_s_waitcnt(0);  // the block's stores issued and complete
+    __syncthreads();
+    st_[3] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && blockIdx.x < W4W_NSTAMP) {
+      unsigned long long* o = g_w4w_stamps[blockIdx.x];
+      o[0] = st_[0], o[1] = st_[1], o[2] = st_[2], o[3] = st_[3];
+      o[8] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID, 32 bits
+      o[9] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID
+    }
+  }
+#endif
 }
 
 // tile groups: the most tiles per group (16 fills every MFMA row), then the widest, among column
@@ -483,6 +522,9 @@ void wino4w_transform_weights(const double* w, int cout, int cin, int cout_p, in
 }
 
 #ifdef CLASFV_KNOCKOUTS
+void wino4w_stamps(unsigned long long* out, int n) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4w_stamps), sizeof(unsigned long long) * 10 * (n < W4W_NSTAMP ? n : W4W_NSTAMP));
+}
 // tools/convbench: conv_wino4w timing knock-outs (KO bits above; 1024: conv_wino4's tile-group rule).
 hipError_t launch_wino4w_ko(const ConvParams& p, hipStream_t s, int ko) {
   if (!wino4w_supported(p) || wino4w_ntn(p.Cout) != 9) return hipErrorInvalidValue;
@@ -500,6 +542,7 @@ hipError_t launch_wino4w_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 15: return launch_w4w_dpw<9, 15>(p, g, nb, s);
     case 128: return launch_w4w_dpw<9, 128>(p, g, nb, s);
     case 256: return launch_w4w_dpw<9, 256>(p, g, nb, s);
+    case 512: return launch_w4w_dpw<9, 512>(p, g, nb, s);
     default: return launch_w4w_dpw<9>(p, g, nb, s);
   }
 }

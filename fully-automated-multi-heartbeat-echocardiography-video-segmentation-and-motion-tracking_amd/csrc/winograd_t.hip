@@ -453,6 +453,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float* res = reinterpret_cast<const float*>(p.res);
   float* yout = SPLIT ? p.part + (size_t)split * ((size_t)p.N * T * HW * CO) : reinterpret_cast<float*>(p.y);
   const size_t fstride = (size_t)HW * CO;
+  // every N tile's bias before the first store, then one explicit vmcnt(0): a bias load issued after a
+  // store waits for it (vmcnt retires in order; the compiler's waits in the per-tile branches were
+  // vmcnt(0)), so the per-tile form paid the store latency once per (m, N tile)
+  f32x4 bvs[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+    bvs[nt] = (p.bias && !SPLIT) ? *reinterpret_cast<const f32x4*>(p.bias + co0 + 16 * nt + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     const int gc = col0 + c_rd + (COLS ? 16 * m : 0);
@@ -464,7 +472,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int nt = 0; nt < NT; ++nt) {
       const int co = co0 + 16 * nt + 4 * q;
       const size_t o = ((size_t)(n * T + t0) * HW + pix) * CO + co;
-      const f32x4 bv = (p.bias && !SPLIT) ? *reinterpret_cast<const f32x4*>(p.bias + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 bv = bvs[nt];
       f32x4 rv[4];
 #pragma unroll
       for (int a2 = 0; a2 < 4; ++a2)

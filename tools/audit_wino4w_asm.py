@@ -67,9 +67,9 @@ def split_functions(lines):
 
 def audit_function(name, body):
     problems = []
-    # asm statements: (start index, end index) of ;;#ASMSTART .. ;;#ASMEND
+    # asm statements (;;#ASMSTART .. ;;#ASMEND) and the accumulators of their v_mfma, per line
     in_asm = [False] * len(body)
-    acc = set()
+    acc_at = {}  # line -> registers an asm MFMA accumulates into
     i = 0
     while i < len(body):
         if ";;#ASMSTART" in body[i]:
@@ -78,14 +78,13 @@ def audit_function(name, body):
                 in_asm[j] = True
                 s = body[j].split(";")[0].strip()
                 if s.startswith("v_mfma"):
-                    dst = s.split(None, 1)[1].split(",")[0]
-                    acc |= regs_of(dst)
+                    acc_at[j] = regs_of(s.split(None, 1)[1].split(",")[0])
                 j += 1
             in_asm[j] = True
             i = j + 1
         else:
             i += 1
-    if not acc:
+    if not acc_at:
         return problems  # an instantiation with no asm MFMAs (NTN <= W4W_NTA)
     # blocks: a label line starts one
     label = None
@@ -94,35 +93,39 @@ def audit_function(name, body):
         if re.match(r"^\.LBB\w+:", ln):
             label = ln
         in_loop[k] = label is not None and "Loop" in label
-    # each chunk loop (a run of loop blocks; the two-item form has two) and its exit prefix: from the
-    # loop's last line to the next drain statement
-    exits = set()
+    # each chunk loop (a run of loop blocks; the two-item form has two, with their own register
+    # assignment) is checked against the accumulators of ITS asm MFMAs, together with its exit prefix:
+    # from the loop's last line to the next drain statement
     k = 0
     while k < len(body):
-        if in_loop[k]:
-            e = k
-            while e + 1 < len(body) and in_loop[e + 1]:
-                e += 1
-            drain = next((d for d in range(e + 1, len(body)) if in_asm[d] and "s_nop 7" in body[d]), None)
-            if drain is None:
-                problems.append(f"{name}: no w4w_drain nop statement after the chunk loop ending at line {e}")
-                drain = e + 1
-            exits.update(range(e + 1, drain))
-            k = e + 1
-        else:
+        if not in_loop[k]:
             k += 1
-    check = [k for k in range(len(body)) if (in_loop[k] or k in exits) and not in_asm[k]]
-    for k in check:
-        s = body[k].split(";")[0].strip()
-        if not s or s.endswith(":") or s.startswith("."):
             continue
-        hit = regs_of(s) & acc
-        if hit:
-            where = "chunk loop" if in_loop[k] else "loop exit before the drain"
-            problems.append(f"{name}: compiler instruction in the {where} touches asm accumulator "
-                            f"v{min(hit)}: {s}")
-        if s.startswith("scratch_") or re.match(r"buffer_store\w* .*s\[0:3\]", s):
-            problems.append(f"{name}: scratch access: {s}")
+        b = k
+        e = k
+        while e + 1 < len(body) and in_loop[e + 1]:
+            e += 1
+        acc = set().union(*[r for ln, r in acc_at.items() if b <= ln <= e]) if any(b <= ln <= e for ln in acc_at) else set()
+        k = e + 1
+        if not acc:
+            continue  # a loop without asm MFMAs
+        drain = next((d for d in range(e + 1, len(body)) if in_asm[d] and "s_nop 7" in body[d]), None)
+        if drain is None:
+            problems.append(f"{name}: no w4w_drain nop statement after the chunk loop ending at line {e}")
+            drain = e + 1
+        for x in range(b, drain):
+            if in_asm[x]:
+                continue
+            s = body[x].split(";")[0].strip()
+            if not s or s.endswith(":") or s.startswith("."):
+                continue
+            hit = regs_of(s) & acc
+            if hit:
+                where = "chunk loop" if in_loop[x] else "loop exit before the drain"
+                problems.append(f"{name}: compiler instruction in the {where} touches asm accumulator "
+                                f"v{min(hit)}: {s}")
+            if s.startswith("scratch_") or re.match(r"buffer_store\w* .*s\[0:3\]", s):
+                problems.append(f"{name}: scratch access: {s}")
     return problems
 
 

@@ -11,6 +11,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../fully-automated-multi-heartbeat-echocardiography-video-segmentation-and-motion-tracking_amd/csrc/common.h"
@@ -28,6 +29,7 @@ hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_patch32_bf16_epi(const ConvParams& p, hipStream_t s, int epi);
 hipError_t launch_winoq_probe(const ConvParams& p, hipStream_t s, int ko);
 void winos_stamps(unsigned long long* out);
+void wino4w_stamps(unsigned long long* out, int n);
 
 // decoder: N clips of T x H x W, taps at (T, H/2, W/2), (T/2, H/4, W/4), (T/4, H/8), (T/8, H/16)
 static int run_decoder(int N, int T, int H, int W, int iters, const std::vector<int>& kos);
@@ -211,6 +213,47 @@ int main(int argc, char** argv) {
           printf("stamps block %d: consumer wait %llu / %llu (%.3f), producer wait %llu / %llu (%.3f)\n", bl,
                  st[bl][0][0], st[bl][0][1], st[bl][0][1] ? (double)st[bl][0][0] / st[bl][0][1] : 0.0, st[bl][1][0],
                  st[bl][1][1], st[bl][1][1] ? (double)st[bl][1][0] / st[bl][1][1] : 0.0);
+      }
+  if (wino4w)
+    for (int ko : kos)
+      if (ko == 512) {  // conv_wino4w per-block stamps (s_memrealtime, 100 MHz)
+        const bool two = false;
+        CK(hipDeviceSynchronize());
+        launch(ko);
+        CK(hipDeviceSynchronize());
+        const int n = 16384;
+        std::vector<unsigned long long> st((size_t)n * 10);
+        wino4w_stamps(st.data(), n);
+        auto S = [&](int b, int i) { return st[(size_t)b * 10 + i]; };
+        const int last = two ? 6 : 3;
+        int nb = 0;
+        while (nb < n && S(nb, last) != 0) ++nb;
+        double ph[6] = {0, 0, 0, 0, 0, 0}, tot = 0;
+        unsigned long long t_min = ~0ull, t_max = 0;
+        for (int b = 0; b < nb; ++b) {
+          for (int i = 0; i < last; ++i) ph[i] += (double)S(b, i + 1) - (double)S(b, i);
+          tot += S(b, last) - S(b, 0);
+          t_min = S(b, 0) < t_min ? S(b, 0) : t_min;
+          t_max = S(b, last) > t_max ? S(b, last) : t_max;
+        }
+        std::vector<int> idx(nb);
+        for (int b = 0; b < nb; ++b) idx[b] = b;
+        auto key = [&](int b) { return (S(b, 9) & 0xf) * 65536 + ((S(b, 8) >> 8) & 0xff); };
+        std::sort(idx.begin(), idx.end(), [&](int a, int b) { return key(a) != key(b) ? key(a) < key(b) : S(a, 0) < S(b, 0); });
+        double gap = 0;
+        int ng = 0, ncu = 0;
+        for (int i = 0; i < nb; ++i) {
+          if (i == 0 || key(idx[i]) != key(idx[i - 1])) {
+            ++ncu;
+            continue;
+          }
+          gap += (double)S(idx[i], 0) - (double)S(idx[i - 1], last);
+          ++ng;
+        }
+        printf("stamps ko %d: %d blocks on %d CUs, wall %.1f us; per block (us):", ko, nb, ncu, (t_max - t_min) / 100.0);
+        const char* names[6] = {"prologue", "chunk loop", "epilogue", "item-2 prologue", "item-2 chunk loop", "item-2 epilogue"};
+        for (int i = 0; i < last; ++i) printf(" %s %.2f,", names[i], ph[i] / nb / 100.0);
+        printf(" total %.2f; CU gap between blocks %.2f us\n", tot / nb / 100.0, ng ? gap / ng / 100.0 : 0.0);
       }
   for (size_t v = 0; v < kos.size(); ++v)
     printf("%s%s%-6s N=%d T=%d H=%d W=%d Cin=%d Cout=%d ko=%-3d  %8.3f ms  %7.1f TF(alg)\n", p.res ? "res   " : "nores ", bf ? "bf16 " : "",
