@@ -806,6 +806,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   }
   __syncthreads();
   const int b_rd = l16 * ROW + ((q ^ (l16 & 3)) << 4);
+  // the bias vectors once per block, not per item: a load issued after an item's stores would wait
+  // for them (vmcnt retires in order)
+  f32x4 bv[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) bv[j] = *reinterpret_cast<const f32x4*>(p.bias + 16 * j + 4 * q);
 #pragma unroll 1
   for (int item = i_start + (int)(blockIdx.x >> 3); item < i_end; item += i_step) {
     const int m0 = item * 256 + wid * 64;
@@ -873,7 +878,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int n = 16 * j + 4 * q;
-        f32x4 v = acc[i][j] + *reinterpret_cast<const f32x4*>(p.bias + n);
+        f32x4 v = acc[i][j] + bv[j];
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = relu1(v[e]);
         *reinterpret_cast<bf16x4*>(y + m * 64 + n) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};

@@ -296,9 +296,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
         for (int j = 0; j < NT; ++j)
           *reinterpret_cast<bf16x4*>(st + (16 * (i - i0) + l16) * VS + (16 * j + 4 * q) * 2) = finish(i, j, gm);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
       __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
       // the pass's 16 MH voxels: block voxel mp + v (v < 16 MH), frame f = mp >> 6 of the block, pixel
       // px0 + v of its 64 (spatial: rows px0 / 8 + v / 8 of the 8x8 tile, column v % 8); store
       // addresses = a wave-uniform base + a small per-lane offset, masks only on edge tiles
@@ -326,9 +326,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
         }
         if (ok) *reinterpret_cast<bf16x8*>(yb + lo) = val;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
       __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     }
   }
 }
@@ -628,7 +628,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   auto finish = [&](int rb, int cb, int g, size_t gm) __attribute__((always_inline)) {
     const int n = n0 + 32 * rb + 8 * g + 4 * h;
     f32x4 v = {acc[rb][cb][4 * g], acc[rb][cb][4 * g + 1], acc[rb][cb][4 * g + 2], acc[rb][cb][4 * g + 3]};
-    if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
+    // p.bias is required (patch32_bf16_supported): an unguarded load, so a column block's loads issue
+    // together (one vmcnt wait) instead of one guarded load and wait each
+    v += *reinterpret_cast<const f32x4*>(p.bias + n);
     if constexpr (RES) {
       const bf16x4 rv = *reinterpret_cast<const bf16x4*>(res + gm * p.Cout + n);
       v += f32x4{(float)rv[0], (float)rv[1], (float)rv[2], (float)rv[3]};
@@ -683,9 +685,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
 #pragma unroll
         for (int g = 0; g < 4; ++g)
           *reinterpret_cast<bf16x4*>(st + vox * VS + (32 * rb + 8 * g + 4 * h) * 2) = finish(rb, cb, g, gm_l);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
       __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
       __bf16* yb = y + ((((size_t)clip * p.To + to) * p.Ho + h0 + 4 * cb) * p.Wo + w0) * p.Cout + n0;
 #pragma unroll
       for (int k = 0; k < INS; ++k) {
@@ -701,9 +703,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
           }
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
       __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     }
   }
 }
@@ -753,7 +755,7 @@ int patch32_pick_nb(const ConvParams& p, int force_nb) {
 }  // namespace
 
 bool patch32_bf16_supported(const ConvParams& p) {
-  if (!p.in_bf16 || !p.out_bf16 || p.stem || p.x2) return false;
+  if (!p.in_bf16 || !p.out_bf16 || p.stem || p.x2 || !p.bias) return false;
   if (p.st != 1 || p.sh != 1 || p.sw != 1) return false;
   if (!(p.KT == 1 && p.KH == 3 && p.KW == 3 && p.pt == 0 && p.ph == 1 && p.pw == 1)) return false;
   if (p.Cin % 32 || p.Kp != 9 * p.Cin) return false;
