@@ -125,6 +125,10 @@ hipError_t launch_wino4w(const ConvParams& p, hipStream_t s);
 double wino4w_exec_gflop(const ConvParams& p);
 void wino4w_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 size_t wino4w_weight_floats(int cin_p, int cout_p);  // 0: no wide block for this cout_p
+// conv_wino4r: conv_wino4w's arithmetic on 12 row waves per block (3 per SIMD), its own U layout
+hipError_t launch_wino4r(const ConvParams& p, hipStream_t s);
+void wino4r_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
+size_t wino4r_weight_floats(int cin_p, int cout_p);
 // Fused Winograd F(4,3)-in-time path for stride-1 3x1x1 fp32 convs; p.w = transformed weights.
 bool winot_supported(const ConvParams& p);
 hipError_t launch_winot(const ConvParams& p, hipStream_t s);

@@ -80,6 +80,7 @@ struct Conv {
   float* dwino = nullptr;  // Winograd F(2x2,3x3) transformed weights (fp32 stride-1 1x3x3 convs)
   float* dwino4 = nullptr;  // Winograd F(4x4,3x3) transformed weights (the same convs, cout_p % 48 == 0)
   float* dwino4w = nullptr;  // the same for conv_wino4w's wide output-channel blocks (wino4w_ntn(cout_p) > 0)
+  float* dwino4r = nullptr;  // the same values in conv_wino4r's (12 row waves) order
   float* dwinot = nullptr;  // Winograd F(4,3)-in-time transformed weights (fp32 stride-1 3x1x1 convs)
   void* dws16 = nullptr;    // bf16 stem weights, hi and lo images [64][7 kh][8 kw][4 c] (bf16 engines);
                             // fp32 engines: hi, mid and lo images [48][7][8][4] (conv_stem_x3)
@@ -122,6 +123,7 @@ int env_variants() {
   if (on("CLASFV_NO_WINO4W")) f |= CLASFV_VARIANT_NO_WINO4W;
   if (on("CLASFV_NO_PATCH32")) f |= CLASFV_VARIANT_NO_PATCH32;
   if (on("CLASFV_NO_PROJ_X3")) f |= CLASFV_VARIANT_NO_PROJ_X3;
+  if (on("CLASFV_NO_WINO4R")) f |= CLASFV_VARIANT_NO_WINO4R;
   return f;
 }
 
@@ -345,11 +347,11 @@ double conv_gflop(const Conv& c, const Shape5& out) {
 double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
   const double nt = (double)out.n * out.t;
   const double cc = (double)c.cin_p * c.cout_p;
-  if (!strcmp(kname, "conv_wino4") || !strcmp(kname, "conv_wino4w")) {  // F(4x4,3x3): 36 products per 4x4
+  if (!strcmp(kname, "conv_wino4") || !strcmp(kname, "conv_wino4w") || !strcmp(kname, "conv_wino4r")) {  // F(4x4,3x3): 36 products per 4x4
     ConvParams p{};                                                           // tile and channel pair, 16-tile groups
     p.N = out.n, p.Ti = p.To = out.t, p.Hi = p.Ho = out.h, p.Wi = p.Wo = out.w;
     p.Cin = c.cin_p, p.Cout = c.cout_p;
-    return kname[10] == 'w' ? wino4w_exec_gflop(p) : wino4_exec_gflop(p);
+    return kname[10] ? wino4w_exec_gflop(p) : wino4_exec_gflop(p);  // conv_wino4r: conv_wino4w's groups
   }
   if (!strcmp(kname, "conv_wino_q") || !strcmp(kname, "conv_wino"))
     return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 1) / 2) * 16.0 * cc * 1e-9;
@@ -409,7 +411,7 @@ const char* pick_kernel(const Conv& c, ConvParams p) {
   // shape rule
   if (c.dwino4 && c.dx3 && p.Ho * p.Wo <= 64 && !p.y_c8 && dma_x3_supported(p)) return "conv_dma_x3";
   if (c.dwino4w && !(p.vflags & (CLASFV_VARIANT_NO_WINO4 | CLASFV_VARIANT_NO_WINO4W)) && wino4w_supported(p))
-    return "conv_wino4w";
+    return c.dwino4r && !(p.vflags & CLASFV_VARIANT_NO_WINO4R) ? "conv_wino4r" : "conv_wino4w";
   if (c.dwino4 && !(p.vflags & CLASFV_VARIANT_NO_WINO4) && wino4_supported(p)) return "conv_wino4";
   if (c.dwino) {
     const bool no_patch = (p.vflags & CLASFV_VARIANT_NO_WINO_PATCH) != 0;
@@ -446,7 +448,8 @@ bool c8_pair(const Conv& a, const Conv& b, const Shape5& in, const Tuning& tu) {
   // Measured per producer (30 clips, profiles/r02j_*): stem and conv_wino_q (layer1, layer2) write
   // the blocked layout at no cost while the temporal kernels after them gain 7-24 %; conv_wino
   // (layer3) broke even and stays channels-last.
-  const bool writes = !strcmp(ka, "conv_wino4") || !strcmp(ka, "conv_wino4w") || !strcmp(ka, "conv_wino_q") ||
+  const bool writes = !strcmp(ka, "conv_wino4") || !strcmp(ka, "conv_wino4w") || !strcmp(ka, "conv_wino4r") ||
+                      !strcmp(ka, "conv_wino_q") ||
                       !strcmp(ka, "conv_stem_f32") ||
                       !strcmp(ka, "conv_stem_x3");
   return writes && !a.out_bf16 && !strcmp(pick_kernel(b, pb), "conv_winot") && winot_c8_ok(pb);
@@ -469,12 +472,16 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
   p.y_c8 = y_c8;
   const char* k = pick_kernel(c, p);
   *kname = k;
-  const bool c8_out = !strcmp(k, "conv_wino4") || !strcmp(k, "conv_wino4w") || !strcmp(k, "conv_wino_q") ||
+  const bool c8_out = !strcmp(k, "conv_wino4") || !strcmp(k, "conv_wino4w") || !strcmp(k, "conv_wino4r") ||
+                      !strcmp(k, "conv_wino_q") ||
                       !strcmp(k, "conv_stem_f32") ||
                       !strcmp(k, "conv_stem_x3");
   if ((y_c8 && !c8_out) || (x_c8 && strcmp(k, "conv_winot")))
     return fail(CLASFV_EINVAL, "internal: 8-channel-blocked layout on an unsupported kernel");
-  if (!strcmp(k, "conv_wino4w")) {
+  if (!strcmp(k, "conv_wino4r")) {
+    p.w = c.dwino4r;
+    HIP_TRY(launch_wino4r(p, s));
+  } else if (!strcmp(k, "conv_wino4w")) {
     p.w = c.dwino4w;
     HIP_TRY(launch_wino4w(p, s));
   } else if (!strcmp(k, "conv_wino4")) {
@@ -641,6 +648,7 @@ int clasfv_destroy(clasfv_t h) {
     (void)hipFree(c.dwino);
     (void)hipFree(c.dwino4);
     (void)hipFree(c.dwino4w);
+    (void)hipFree(c.dwino4r);
     (void)hipFree(c.dwinot);
     (void)hipFree(c.dws16);
     (void)hipFree(c.dx3);
@@ -712,12 +720,13 @@ int clasfv_finalize(clasfv_t h) {
     (void)hipFree(c.dwino);
     (void)hipFree(c.dwino4);
     (void)hipFree(c.dwino4w);
+    (void)hipFree(c.dwino4r);
     (void)hipFree(c.dwinot);
     (void)hipFree(c.dws16);
     (void)hipFree(c.dx3);
     c.dw = c.dws16 = c.dx3 = nullptr;
     c.db = nullptr;
-    c.dwino = c.dwino4 = c.dwino4w = c.dwinot = nullptr;
+    c.dwino = c.dwino4 = c.dwino4w = c.dwino4r = c.dwinot = nullptr;
     bn_scale_shift(h, c.bn, c.cout, s, t);
     const auto& w = P(h, c.w + ".weight");
     const int taps = c.kt * c.kh * c.kw;
@@ -741,6 +750,9 @@ int clasfv_finalize(clasfv_t h) {
         std::vector<float> uw(wino4w_weight_floats(c.cin_p, c.cout_p));
         wino4w_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, uw.data());
         if ((rc = upload(uw, &c.dwino4w))) return rc;
+        std::vector<float> ur(wino4r_weight_floats(c.cin_p, c.cout_p));
+        wino4r_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, ur.data());
+        if ((rc = upload(ur, &c.dwino4r))) return rc;
       }
     }
     if (!bf16 && c.stem && c.cout_p == 48 && c.kh == 7 && c.kw == 7 && cin <= 4) {  // conv_stem_x3's pieces
@@ -876,7 +888,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0xFFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~0x1FFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;

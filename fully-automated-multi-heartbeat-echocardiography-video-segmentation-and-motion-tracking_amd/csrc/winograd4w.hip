@@ -411,6 +411,384 @@ __global__ __launch_bounds__(W4_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1
 #endif
 }
 
+// ---------------------------------------------------------------------------------------------
+// conv_wino4r (round 5): conv_wino4w's tile groups, U values, products and accumulation order on 12
+// waves per block -- three per SIMD instead of one. Wave (rh, ch, r) owns ONE row i = 3 rh + r of the
+// quadrant (rh, ch): 3 Winograd elements x NTN N tiles = 108 accumulator registers at NTN = 9, so
+// three waves fit a SIMD's 512 registers, and each SIMD interleaves three MFMA streams (the lone
+// conv_wino4w wave issues back to back only where nothing else is in its stream: its chunk loop ran
+// at ≈ 0.75 of the f32 MFMA rate, profiles/r05c_wino4w_stamps.txt). The epilogue exchanges three N
+// tiles per round through three plane buffers (768 unit threads: one (tile, 4 channels, column b)
+// unit of each), 3 rounds instead of 9 at NTN = 9. The cost: each wave reads its window rows of the
+// raw patch itself (3x the transform's LDS reads, ≈ 1.2x its VALU: a row of B^T d is 1/3 of a
+// quadrant's row transform).
+constexpr int W4R_WAVES = 12;
+constexpr int W4R_THREADS = 64 * W4R_WAVES;
+constexpr int W4R_DPW = 2;  // DMA instructions per wave per ring stage (wino4_geometry: NI <= 24)
+constexpr int W4R_STAGE = W4R_WAVES * W4R_DPW * 1024;
+constexpr int W4R_NR = 4, W4R_STEP = 2;  // 4 stages, one barrier per 2 chunks
+constexpr int W4R_NZ = 3;  // epilogue plane buffers = N tiles per epilogue round
+constexpr int W4R_LDS = W4R_NZ * W4W_ZBUF * 4;  // 163,296 B
+static_assert(W4R_LDS >= W4R_NR * W4R_STAGE + 1024 && W4R_LDS <= 160 * 1024, "ring and planes fit LDS");
+
+// per wave and chunk: NV = 3 elements x 2 K steps x NTN U values, m = (nt * 2 + ks) * 3 + jj, as NU f32x4
+// loads through a UQ-deep register ring
+template <int NTN>
+struct W4R {
+  static constexpr int NV = 6 * NTN;
+  static constexpr int UQ = NTN == 9 ? 7 : 9;
+  static constexpr int NU = (NV + 4 * UQ - 1) / (4 * UQ) * UQ;
+};
+
+// row R of bt_rows<RH> (the same expressions, so the same roundings)
+template <int RH, int R>
+__device__ inline f32x2 bt_row(const f32x2 (&e)[5]) {
+  if constexpr (RH == 0) {
+    if constexpr (R == 0) {
+      return e[0] * 4.f - e[2] * 5.f + e[4];
+    } else if constexpr (R == 1) {
+      const f32x2 s = e[1] + e[2], u = e[3] + e[4];
+      return u - s * 4.f;
+    } else {
+      const f32x2 d = e[1] - e[2], w = e[4] - e[3];
+      return w + d * 4.f;
+    }
+  } else {
+    if constexpr (R == 2) {
+      return e[0] * 4.f - e[2] * 5.f + e[4];
+    } else {
+      const f32x2 x = e[3] - e[1], y = e[2] - e[0];
+      if constexpr (R == 0)
+        return x + y * 2.f;
+      else
+        return x - y * 2.f;
+    }
+  }
+}
+
+// KO (tools/convbench diagnostics, 0 in the product): 4 no epilogue, 128 no output stores, 512 per-block
+// phase stamps (as conv_wino4w's)
+template <int NTN, bool C8, int KO = 0, bool RELU = true>
+__global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_wino4r(ConvParams p,
+                                                                                                       W4Geo g) {
+  using WR = W4R<NTN>;
+  constexpr int NR = W4R_NR, STAGE = W4R_STAGE, UQ = WR::UQ, NU = WR::NU, NV = WR::NV;
+  __shared__ __align__(16) char smem[W4R_LDS];
+  char* sink = smem + NR * STAGE;
+
+#ifdef CLASFV_KNOCKOUTS
+  unsigned long long st_[4] = {0, 0, 0, 0};
+  if constexpr ((KO & 512) != 0) st_[0] = __builtin_amdgcn_s_memrealtime();
+#endif
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.x), (short)0, (int)((size_t)p.N * p.Ti * p.Hi * p.Wi * p.Cin * 4), 0x00020000);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int blk = xcd_swizzle4(blockIdx.x, gridDim.x);
+  const int grp = fdiv(blk, g.fd_cob), cob = blk - grp * g.n_cob;
+  const int rg = fdiv(grp, g.fd_gpr), gx = grp - rg * g.gpr;
+  const int R0 = rg * g.TR, tx0 = gx * g.TC;
+  const int H = p.Ho, W = p.Wo, C = p.Cin;
+  const int nchunk = C >> 3;
+  const int NT = g.TR * g.TC;
+  // wave (rh, ch, r) = wid / 6, (wid / 3) % 2, wid % 3
+  const int wq = wid / 3, r = wid - 3 * wq, rh = wq >> 1, ch = wq & 1;
+
+  // ---- LDS-DMA slot table (conv_wino4w's, over 12 waves): instruction j of this wave fills slots
+  // (wid + 12 j) * 64 + lane of a stage
+  unsigned d_off[W4R_DPW];
+#pragma unroll
+  for (int j = 0; j < W4R_DPW; ++j) {
+    const int ins = wid + W4R_WAVES * j, s = ins * 64 + lane;
+    unsigned off = 0x80000000u;
+    if (ins < g.NI && s < 2 * g.RS) {
+      const int hf = s >= g.RS ? 1 : 0, sl = s - hf * g.RS;
+      const int seg = fdiv(sl, g.fd_ss), ss = sl - seg * g.SS;
+      const int rr = fdiv(ss, g.fd_rp), cs = ss - rr * g.RP;
+      const int m5 = cs / 5, k5 = cs - 5 * m5, c = 4 * m5 + k5;
+      if (rr < 6 && k5 < 4 && c < 4 * g.TC + 2) {
+        const int R = R0 + seg, f = fdiv(R, g.fd_th), ty = R - f * g.TH;
+        const int yy = 4 * ty - 1 + rr, xx = 4 * tx0 - 1 + c;
+        if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) off = (((f * H + yy) * W + xx) * C + hf * 4) * 4;
+      }
+    }
+    d_off[j] = off;
+  }
+  auto issue_raw = [&](int k, int stage) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < W4R_DPW; ++j) {
+      const int ins = wid + W4R_WAVES * j;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xr, (__attribute__((address_space(3))) void*)(ins < g.NI ? smem + stage * STAGE + ins * 1024 : sink), 16,
+          d_off[j], k < nchunk ? k * 32 : 0, 0, 0);
+    }
+  };
+
+  // ---- transform lane: tile t, channel pair k4 (conv_wino4w's); this wave's row of B^T d B
+  const int t = lane & 15, k4 = lane >> 4;
+  const int tv = t < NT ? t : 0;
+  const int tseg = fdiv(tv, g.fd_tc), tcol = tv - tseg * g.TC;
+  const int lane_off = ((k4 >> 1) * g.RS + tseg * g.SS + rh * g.RP + 5 * tcol) * 16 + (k4 & 1) * 8;
+  const int rp16 = g.RP * 16;
+  auto transform = [&](int stage, f32x2 (&a)[3]) __attribute__((always_inline)) {
+    if constexpr ((KO & 1) != 0) {
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) a[jj] = f32x2{(float)(lane + jj + stage), (float)(lane - jj)};
+      return;
+    }
+    const char* base = smem + stage * STAGE + lane_off;
+    auto body = [&](auto rh_c, auto ch_c, auto r_c) __attribute__((always_inline)) {
+      constexpr int RH = decltype(rh_c)::value, CH = decltype(ch_c)::value, RR = decltype(r_c)::value;
+      f32x2 tt[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const int co = (c + (c >> 2)) * 16;  // pixel columns 0..5 of the window -> slots 0,1,2,3,5,6
+        f32x2 e[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) e[q] = *reinterpret_cast<const f32x2*>(base + q * rp16 + co);
+        tt[c] = bt_row<RH, RR>(e);
+        // one column's window reads in flight at a time: 168 registers hold 108 accumulators and the
+        // U ring (hoisting every column's reads spilled)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      bt_cols<CH>(tt, a);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    switch (wid) {
+      case 0: body(I0{}, I0{}, I0{}); break;
+      case 1: body(I0{}, I0{}, I1{}); break;
+      case 2: body(I0{}, I0{}, I2{}); break;
+      case 3: body(I0{}, I1{}, I0{}); break;
+      case 4: body(I0{}, I1{}, I1{}); break;
+      case 5: body(I0{}, I1{}, I2{}); break;
+      case 6: body(I1{}, I0{}, I0{}); break;
+      case 7: body(I1{}, I0{}, I1{}); break;
+      case 8: body(I1{}, I0{}, I2{}); break;
+      case 9: body(I1{}, I1{}, I0{}); break;
+      case 10: body(I1{}, I1{}, I1{}); break;
+      default: body(I1{}, I1{}, I2{}); break;
+    }
+  };
+
+  // ---- U operands: [cob][chunk][wave][NU][lane][4] (wino4r_transform_weights)
+  const __amdgpu_buffer_rsrc_t ur = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(reinterpret_cast<const float*>(p.w) + ((size_t)cob * nchunk * W4R_WAVES + wid) * (NU * 256)),
+      (short)0, nchunk * W4R_WAVES * NU * 256 * 4, 0x00020000);
+  auto load_u = [&](int k, int gi) __attribute__((always_inline)) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                         ur, lane * 16, ((k < nchunk ? k : 0) * (W4R_WAVES * NU * 256) + gi * 256) * 4, 0));
+  };
+
+  f32x4 acc[NTN][3];  // [nt][jj]: lane (tile l16, channels 4 q .. 4 q + 3 of N tile nt), element (i, 3 ch + jj)
+#pragma unroll
+  for (int nt = 0; nt < NTN; ++nt)
+#pragma unroll
+    for (int jj = 0; jj < 3; ++jj) acc[nt][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 u[UQ];
+  f32x2 a[3];
+
+  issue_raw(0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  issue_raw(1, 1);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int gi = 0; gi < UQ; ++gi) u[gi] = load_u(0, gi);
+  __builtin_amdgcn_sched_barrier(0);
+
+  // the ring and wait rule of conv_wino4w at NR = 4: every 2 chunks a barrier, then raw(k + 2),
+  // raw(k + 3) into the stages of chunks k - 2, k - 1; at most UQ VMEM ops outstanding at the wait
+  // (the U loads issued after raw(k + 1) on chunk 0, 2 NU later) leaves raw(k), raw(k + 1) landed
+  int k = 0;
+#pragma unroll 1
+  do {
+    const int ph = k % NR;
+    if (ph % W4R_STEP == 0) {
+      __builtin_amdgcn_s_waitcnt(vm_wait(UQ));
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((KO & 16) == 0) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+#ifdef CLASFV_KNOCKOUTS
+      if constexpr ((KO & 512) != 0)
+        if (k == 0) st_[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+      if constexpr ((KO & 8) == 0) {
+#pragma unroll
+        for (int d = 2; d < NR; ++d) issue_raw(k + d, (ph + d) % NR);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    transform(ph, a);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int gi = 0; gi < NU; ++gi) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int m = 4 * gi + c;
+        if (m < NV) {
+          const int jj = m % 3, ks = (m / 3) % 2, nt = m / 6;
+          acc[nt][jj] = __builtin_amdgcn_mfma_f32_16x16x4f32(u[gi % UQ][c], ks ? a[jj].y : a[jj].x, acc[nt][jj], 0, 0, 0);
+        }
+      }
+      if constexpr ((KO & 2) == 0) {
+        const int gn = gi + UQ;
+        u[gi % UQ] = gn < NU ? load_u(k, gn) : load_u(k + 1, gn - NU);
+      }
+    }
+    constexpr int FG = NV / 4, RM = NV % 4;
+#pragma unroll
+    for (int gi = 0; gi < NU; ++gi) {
+      if (gi < FG)
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMA
+      else if (gi == FG && RM)
+        __builtin_amdgcn_sched_group_barrier(0x008, RM, 0);
+      if constexpr ((KO & 2) == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+    }
+  } while (++k < nchunk);
+  __builtin_amdgcn_s_waitcnt(vm_wait(0));
+  __syncthreads();
+#ifdef CLASFV_KNOCKOUTS
+  if constexpr ((KO & 512) != 0) st_[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+
+  if constexpr ((KO & 4) != 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int nt = 0; nt < NTN; ++nt)
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) sum += acc[nt][jj][0] + acc[nt][jj][3];
+    if (sum == 1234.5f) reinterpret_cast<float*>(p.y)[tid] = sum;
+    return;
+  }
+  // ---- epilogue: conv_wino4w's planes and output transform, W4R_NZ N tiles per round: every wave
+  // writes its row's planes of the round's N tiles into buffers 0..2, then thread (ug, unit) reads,
+  // transforms and stores unit `unit` of N tile 3 round + ug
+  float* Z0 = reinterpret_cast<float*>(smem);
+  const int q = lane >> 4, l16 = lane & 15;
+  const size_t plane = (size_t)p.N * p.To * H * W * 8;
+  float* yout = reinterpret_cast<float*>(p.y);
+  const int ug = tid >> 8, ut = tid & 255;
+  const int ub = ut & 3, ucq = (ut >> 2) & 3, utile = ut >> 4;
+  const int useg = fdiv(utile, g.fd_tc), utc = utile - useg * g.TC;
+  const int uR = R0 + useg, uf = fdiv(uR, g.fd_th), uty = uR - uf * g.TH;
+  const int uxx = 4 * (tx0 + utc) + ub;
+  const bool ulive = utile < NT && uxx < W;
+  const int eb = ub == 3 ? 1 : ub;
+  const int CO = p.Cout;
+  const int zrow = 3 * rh + r;
+  auto write_planes = [&](int nt, int buf) __attribute__((always_inline)) {
+    float* Z = Z0 + buf * W4W_ZBUF;
+    const f32x4 m0 = acc[nt][0], m1 = acc[nt][1], m2 = acc[nt][2];
+    if (ch == 0) {
+      f32x4* zp = reinterpret_cast<f32x4*>(Z + (zrow * 3) * W4W_ZP + l16 * W4W_ZT + 4 * q);
+      zp[0] = m0 + m1 + m2;
+      zp[W4W_ZP / 4] = psub4(m1, m2);
+      zp[2 * W4W_ZP / 4] = m1 + m2;
+    } else {
+      f32x4* zp = reinterpret_cast<f32x4*>(Z + (18 + zrow * 4) * W4W_ZP + l16 * W4W_ZT + 4 * q);
+      const f32x4 sm = m0 + m1, df = psub4(m0, m1);
+      zp[0] = sm;
+      zp[W4W_ZP / 4] = 2.f * df;
+      zp[2 * W4W_ZP / 4] = 4.f * sm;
+      zp[3 * W4W_ZP / 4] = 8.f * df + m2;
+    }
+  };
+  auto read_unit = [&](int buf, f32x4 (&P)[6]) __attribute__((always_inline)) {
+    const float* Z = Z0 + buf * W4W_ZBUF;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+      P[i] = *reinterpret_cast<const f32x4*>(Z + (i * 3 + eb) * W4W_ZP + utile * W4W_ZT + 4 * ucq) +
+             *reinterpret_cast<const f32x4*>(Z + (18 + i * 4 + ub) * W4W_ZP + utile * W4W_ZT + 4 * ucq);
+  };
+  const int co0 = cob * NTN * 16 + 4 * ucq;
+  const size_t upix = (size_t)(uf * H + 4 * uty) * W + uxx;
+  float* ybase[4];
+#pragma unroll
+  for (int aa = 0; aa < 4; ++aa) {
+    const size_t px = upix + (size_t)aa * W;
+    ybase[aa] = yout + (C8 ? (size_t)(co0 >> 3) * plane + px * 8 + (co0 & 7) : px * CO + co0);
+  }
+  const size_t nt_step = C8 ? 2 * plane : 16;
+  constexpr int NRND = (NTN + W4R_NZ - 1) / W4R_NZ;
+  // this thread's N tiles' bias, loaded before the first store (conv_wino4w's reason)
+  f32x4 biasv[NRND];
+#pragma unroll
+  for (int rd = 0; rd < NRND; ++rd) {
+    const int nt = W4R_NZ * rd + ug;
+    biasv[rd] = p.bias && nt < NTN ? *reinterpret_cast<const f32x4*>(p.bias + co0 + nt * 16) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  auto store_unit = [&](int nt, const f32x4& bias, const f32x4 (&P)[6]) __attribute__((always_inline)) {
+    const f32x4 s12 = P[1] + P[2], d12 = psub4(P[1], P[2]), s34 = P[3] + P[4], d34 = psub4(P[3], P[4]);
+    f32x4 y[4];
+    y[0] = P[0] + s12 + s34;
+    y[1] = d12 + 2.f * d34;
+    y[2] = s12 + 4.f * s34;
+    y[3] = d12 + 8.f * d34 + P[5];
+#pragma unroll
+    for (int aa = 0; aa < 4; ++aa) {
+      if (4 * uty + aa >= H) break;
+      f32x4 o = y[aa] + bias;
+      if constexpr (RELU) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) o[c] = relu1(o[c]);
+      }
+      float* dst = ybase[aa] + nt * nt_step;
+      if constexpr ((KO & 128) != 0) {
+        if (o[0] == 1234.5f) *reinterpret_cast<f32x4*>(dst) = o;
+      } else {
+        *reinterpret_cast<f32x4*>(dst) = o;
+      }
+    }
+  };
+#pragma unroll
+  for (int b = 0; b < W4R_NZ; ++b)
+    if (b < NTN) write_planes(b, b);
+#pragma unroll
+  for (int rd = 0; rd < NRND; ++rd) {
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    const int nt_u = W4R_NZ * rd + ug;
+    const bool live = ulive && nt_u < NTN;
+    f32x4 P[6];
+    if (live) read_unit(ug, P);
+    if (rd + 1 < NRND) {
+      __syncthreads();
+#pragma unroll
+      for (int b = 0; b < W4R_NZ; ++b)
+        if (W4R_NZ * (rd + 1) + b < NTN) write_planes(W4R_NZ * (rd + 1) + b, b);
+    }
+    if (live) store_unit(nt_u, biasv[rd], P);
+  }
+#ifdef CLASFV_KNOCKOUTS
+  if constexpr ((KO & 512) != 0) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    st_[3] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && blockIdx.x < W4W_NSTAMP) {
+      unsigned long long* o = g_w4w_stamps[blockIdx.x];
+      o[0] = st_[0], o[1] = st_[1], o[2] = st_[2], o[3] = st_[3];
+      o[8] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+      o[9] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+    }
+  }
+#endif
+}
+
+template <int NTN, int KO = 0>
+hipError_t launch_w4r(const ConvParams& p, const W4Geo& g, int n_blocks, hipStream_t s) {
+  const dim3 grid(n_blocks), block(W4R_THREADS);
+  if (p.y_c8 && p.relu)
+    hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, true>), grid, block, 0, s, p, g);
+  else if (p.relu)
+    hipLaunchKernelGGL((conv_wino4r<NTN, false, KO, true>), grid, block, 0, s, p, g);
+  else if (p.y_c8)
+    hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, false>), grid, block, 0, s, p, g);
+  else
+    hipLaunchKernelGGL((conv_wino4r<NTN, false, KO, false>), grid, block, 0, s, p, g);
+  return hipGetLastError();
+}
+
 // tile groups: the most tiles per group (16 fills every MFMA row), then the widest, among column
 // widths >= W4W_FILL (56x56 maps: 8 x 2 tiles, 28x28: 16 x 1)
 // (profiles/r04_wino4w_fill16.txt)
@@ -521,6 +899,57 @@ void wino4w_transform_weights(const double* w, int cout, int cin, int cout_p, in
     }
 }
 
+// conv_wino4r (12 row waves per block) on conv_wino4w's tile groups; p.w: wino4r_transform_weights' layout.
+hipError_t launch_wino4r(const ConvParams& p, hipStream_t s) {
+  if (!wino4w_supported(p)) return hipErrorInvalidValue;
+  W4Geo g;
+  int nb;
+  const int ntn = wino4w_ntn(p.Cout);
+  wino4_geometry(p, &g, &nb, 16 * ntn, W4W_FILL);
+  return ntn == 9 ? launch_w4r<9>(p, g, nb, s) : launch_w4r<6>(p, g, nb, s);
+}
+
+size_t wino4r_weight_floats(int cin_p, int cout_p) {
+  const int ntn = wino4w_ntn(cout_p);
+  if (!ntn) return 0;
+  const int nu = ntn == 9 ? W4R<9>::NU : W4R<6>::NU;
+  return (size_t)(cout_p / (16 * ntn)) * (cin_p / 8) * W4R_WAVES * nu * 256;
+}
+
+// U[cout_p/(16 NTN)][cin_p/8][12 waves][NU][64 lane][4]: wave (rh, ch, r) = (w / 6, (w / 3) % 2, w % 3),
+// lane = k4 * 16 + n, value m = 4 group + comp = (nt * 2 + ks) * 3 + jj (m >= 6 NTN: zero): element
+// (3 rh + r, 3 ch + jj) of G g G^T (conv_wino4w's values, double on the host) for input channel
+// chunk * 8 + 2 k4 + ks and output channel cob * 16 NTN + nt * 16 + n.
+void wino4r_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U) {
+  static const double G[6][3] = {{1.0 / 4, 0, 0},
+                                 {-1.0 / 6, -1.0 / 6, -1.0 / 6},
+                                 {-1.0 / 6, 1.0 / 6, -1.0 / 6},
+                                 {1.0 / 24, 1.0 / 12, 1.0 / 6},
+                                 {1.0 / 24, -1.0 / 12, 1.0 / 6},
+                                 {0, 0, 1}};
+  const int ntn = wino4w_ntn(cout_p);
+  const int nu = ntn == 9 ? W4R<9>::NU : W4R<6>::NU;
+  const int nch = cin_p / 8, cw = 16 * ntn;
+  const size_t total = wino4r_weight_floats(cin_p, cout_p);
+  for (size_t i = 0; i < total; ++i) U[i] = 0.f;
+  for (int o = 0; o < cout; ++o)
+    for (int c = 0; c < cin; ++c) {
+      const double* gw = w + ((size_t)o * cin + c) * 9;
+      double tmp[6][3];
+      for (int i = 0; i < 6; ++i)
+        for (int v = 0; v < 3; ++v) tmp[i][v] = G[i][0] * gw[0 * 3 + v] + G[i][1] * gw[1 * 3 + v] + G[i][2] * gw[2 * 3 + v];
+      const int cob = o / cw, nt = (o % cw) / 16, n = o % 16;
+      const int chunk = c / 8, k4 = (c % 8) / 2, ks = c % 2;
+      for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+          const double uu = tmp[i][0] * G[j][0] + tmp[i][1] * G[j][1] + tmp[i][2] * G[j][2];
+          const int wv = ((i / 3) * 2 + j / 3) * 3 + i % 3, jj = j % 3;
+          const int m = (nt * 2 + ks) * 3 + jj, gi = m / 4, comp = m % 4;
+          U[((((((size_t)cob * nch + chunk) * W4R_WAVES + wv) * nu + gi) * 64) + k4 * 16 + n) * 4 + comp] = (float)uu;
+        }
+    }
+}
+
 #ifdef CLASFV_KNOCKOUTS
 void wino4w_stamps(unsigned long long* out, int n) {
   (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_w4w_stamps), sizeof(unsigned long long) * 10 * (n < W4W_NSTAMP ? n : W4W_NSTAMP));
@@ -545,5 +974,42 @@ hipError_t launch_wino4w_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 512: return launch_w4w_dpw<9, 512>(p, g, nb, s);
     default: return launch_w4w_dpw<9>(p, g, nb, s);
   }
+}
+// tools/convbench: conv_wino4r diagnostics (KO bits 4, 128, 512 of conv_wino4r), NTN = 9 only
+hipError_t launch_wino4r_ko(const ConvParams& p, hipStream_t s, int ko) {
+  if (!wino4w_supported(p) || wino4w_ntn(p.Cout) != 9) return hipErrorInvalidValue;
+  W4Geo g;
+  int nb;
+  wino4_geometry(p, &g, &nb, 144, W4W_FILL);
+  switch (ko) {
+    case 1: return launch_w4r<9, 1>(p, g, nb, s);
+    case 2: return launch_w4r<9, 2>(p, g, nb, s);
+    case 8: return launch_w4r<9, 8>(p, g, nb, s);
+    case 16: return launch_w4r<9, 16>(p, g, nb, s);
+    case 31: return launch_w4r<9, 31>(p, g, nb, s);
+    case 4: return launch_w4r<9, 4>(p, g, nb, s);
+    case 128: return launch_w4r<9, 128>(p, g, nb, s);
+    case 512: return launch_w4r<9, 512>(p, g, nb, s);
+    default: return launch_w4r<9>(p, g, nb, s);
+  }
+}
+// the wino4r image of a conv_wino4w image (a permutation: the same U values in wino4r's order)
+void wino4r_from_wino4w(const float* Uw, int cin_p, int cout_p, float* Ur) {
+  const int ntn = wino4w_ntn(cout_p);
+  const int nuw = ntn == 9 ? W4W<9>::NU : W4W<6>::NU, nur = ntn == 9 ? W4R<9>::NU : W4R<6>::NU;
+  const int nch = cin_p / 8, ncob = cout_p / (16 * ntn);
+  for (size_t i = 0; i < wino4r_weight_floats(cin_p, cout_p); ++i) Ur[i] = 0.f;
+  for (int cob = 0; cob < ncob; ++cob)
+    for (int ck = 0; ck < nch; ++ck)
+      for (int wv = 0; wv < 4; ++wv)
+        for (int r = 0; r < 3; ++r)
+          for (int nt = 0; nt < ntn; ++nt)
+            for (int ks = 0; ks < 2; ++ks)
+              for (int jj = 0; jj < 3; ++jj) {
+                const int mw = ((nt * 3 + r) * 2 + ks) * 3 + jj, mr = (nt * 2 + ks) * 3 + jj;
+                for (int l = 0; l < 64; ++l)
+                  Ur[(((((size_t)cob * nch + ck) * W4R_WAVES + wv * 3 + r) * nur + mr / 4) * 64 + l) * 4 + mr % 4] =
+                      Uw[(((((size_t)cob * nch + ck) * 4 + wv) * nuw + mw / 4) * 64 + l) * 4 + mw % 4];
+              }
 }
 #endif

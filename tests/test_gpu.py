@@ -620,20 +620,27 @@ def test_wino4_matches_wino2(model, shape):
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (3, 3, 24, 32, 32), (2, 3, 16, 64, 48),
                                    (1, 3, 16, 112, 224)])
 def test_wino4w_bitexact_vs_wino4(model, shape):
-    """conv_wino4w (wide output-channel blocks: 144 / 288 / 576 channels as 144-channel blocks, 480 as
-    96; 240 stays on conv_wino4) issues conv_wino4's products in conv_wino4's order (variant
-    no_wino4w): the forward is bit-identical, with the wide kernel really running."""
+    """The wide-block F(4x4,3x3) kernels issue conv_wino4's products in conv_wino4's order, so the
+    forward is bit-identical across all three, with each kernel really running: conv_wino4r (the
+    default: 12 row waves per block, three per SIMD; winograd4w.hip), conv_wino4w (variant no_wino4r:
+    4 quadrant waves, one per SIMD) and conv_wino4 (variant no_wino4w: 48-channel blocks). Wide blocks
+    cover 144 / 288 / 576 channels as 144-channel blocks and 480 as 96; 240 stays on conv_wino4."""
     rng = np.random.default_rng(47)
     x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
-    model.engine.set_kernel_timing(True)
-    s_w, m_w = model(x)
-    kt = model.engine.kernel_timing()
-    model.engine.set_kernel_timing(False)
-    assert "conv_wino4w" in kt
-    model.set_kernel_variants("no_wino4w")
-    s_4, m_4 = model(x)
-    model.set_kernel_variants()
-    assert torch.equal(s_w, s_4) and torch.equal(m_w, m_4)
+    outs = []
+    for variant, kernel in ((None, "conv_wino4r"), ("no_wino4r", "conv_wino4w"), ("no_wino4w", "conv_wino4")):
+        if variant:
+            model.set_kernel_variants(variant)
+        model.engine.set_kernel_timing(True)
+        outs.append(model(x))
+        kt = model.engine.kernel_timing()
+        model.engine.set_kernel_timing(False)
+        model.set_kernel_variants()
+        assert kernel in kt, (variant, sorted(kt))
+        if kernel != "conv_wino4":
+            assert "conv_wino4r" not in kt or "conv_wino4w" not in kt
+    for s_v, m_v in outs[1:]:
+        assert torch.equal(outs[0][0], s_v) and torch.equal(outs[0][1], m_v)
 
 
 @pytest.mark.parametrize("shape", [(1, 3, 32, 112, 112), (2, 3, 16, 64, 48), (3, 3, 8, 32, 32)])

@@ -30,6 +30,8 @@ hipError_t launch_patch32_bf16_epi(const ConvParams& p, hipStream_t s, int epi);
 hipError_t launch_winoq_probe(const ConvParams& p, hipStream_t s, int ko);
 void winos_stamps(unsigned long long* out);
 void wino4w_stamps(unsigned long long* out, int n);
+hipError_t launch_wino4r_ko(const ConvParams& p, hipStream_t s, int ko);
+void wino4r_from_wino4w(const float* Uw, int cin_p, int cout_p, float* Ur);
 
 // decoder: N clips of T x H x W, taps at (T, H/2, W/2), (T/2, H/4, W/4), (T/4, H/8), (T/8, H/16)
 static int run_decoder(int N, int T, int H, int W, int iters, const std::vector<int>& kos);
@@ -93,7 +95,10 @@ int main(int argc, char** argv) {
   const bool winoqp = !strcmp(kind, "winoqp");  // conv_wino_q knock-out probes (tools/winoq_probe.hip)
   const bool winoq = !strcmp(kind, "winoq") || winoqp, winor = !strcmp(kind, "winor");
   const bool wino4 = !strcmp(kind, "wino4");  // conv_wino4 (F(4x4,3x3); no residual)
-  const bool wino4w = !strcmp(kind, "wino4w");  // conv_wino4w (wide blocks; ko: knock-outs at NTN 9)
+  // conv_wino4r (12 row waves): ko bits as conv_wino4r's; ko + 8192: conv_wino4w (ko - 8192) on the same
+  // U values (the wino4w image, permuted for wino4r)
+  const bool wino4r = !strcmp(kind, "wino4r");
+  const bool wino4w = !strcmp(kind, "wino4w") || wino4r;  // conv_wino4w (wide blocks; ko: knock-outs at NTN 9)
   const bool wino = !strcmp(kind, "wino") || winoq || winor || wino4 || wino4w, winot = !strcmp(kind, "winot");
   const bool spp = !strcmp(kind, "spp"), tpp = !strcmp(kind, "tpp");  // bf16 patch-staged (conv_patch.hip)
   const bool sp = wino || spp || !strcmp(kind, "sp"), tp = winot || tpp || !strcmp(kind, "tp");
@@ -125,6 +130,14 @@ int main(int argc, char** argv) {
   p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
   p.res = (getenv("CB_NORES") || wino4 || wino4w) ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
   CK(hipMalloc(&p.y, ny * 4));
+  void* w4r = nullptr;
+  if (wino4r) {
+    std::vector<float> uw(nw), urr(wino4r_weight_floats(Cin, Cout));
+    CK(hipMemcpy(uw.data(), p.w, nw * 4, hipMemcpyDeviceToHost));
+    wino4r_from_wino4w(uw.data(), Cin, Cout, urr.data());
+    CK(hipMalloc(&w4r, urr.size() * 4));
+    CK(hipMemcpy(w4r, urr.data(), urr.size() * 4, hipMemcpyHostToDevice));
+  }
   // ko 710..719 (fp32 direct convs): conv_dma_x3 on the split-bf16 image of the same weights,
   // split-K into ko - 710 K ranges when >= 2
   void* wx3 = nullptr;
@@ -151,7 +164,14 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   auto launch = [&](int ko) {
-    if (wino4w) CK(ko ? launch_wino4w_ko(p, s, ko) : launch_wino4w(p, s));
+    if (wino4r && !(ko & 8192)) {
+      ConvParams q = p;
+      q.w = w4r;
+      CK(ko ? launch_wino4r_ko(q, s, ko) : launch_wino4r(q, s));
+    } else if (wino4w) {
+      const int kw = ko & ~8192;
+      CK(kw ? launch_wino4w_ko(p, s, kw) : launch_wino4w(p, s));
+    }
     else if (wino4) CK(ko ? launch_wino4_ko(p, s, ko) : launch_wino4(p, s));
     else if (winor) CK(launch_winor_ko(p, s, ko));
     else if (winoqp) CK(launch_winoq_probe(p, s, ko));
@@ -216,7 +236,7 @@ int main(int argc, char** argv) {
       }
   if (wino4w)
     for (int ko : kos)
-      if (ko == 512) {  // conv_wino4w per-block stamps (s_memrealtime, 100 MHz)
+      if ((ko & ~8192) == 512) {  // conv_wino4w / conv_wino4r per-block stamps (s_memrealtime, 100 MHz)
         const bool two = false;
         CK(hipDeviceSynchronize());
         launch(ko);
