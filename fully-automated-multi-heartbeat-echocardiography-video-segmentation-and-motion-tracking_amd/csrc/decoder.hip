@@ -31,26 +31,33 @@ namespace {
 // pixel px, channel group q) slots at 16-B quad (px * PIX / 4 + q) mod 16 = (2 px + q) mod 16: all
 // distinct for the 2x-upsampled tap (PIX = 68 gave (px + q) mod 16, 2-way conflicts).
 constexpr int PIX = 72;
-constexpr int TILE_H = 8, TILE_W = 16;
-// Source window bounds of one 8x16-voxel tile per tap (tap i: scale (in-1)/(out-1) < 2^-(i+1), so
-// 8 rows touch at most floor(7 s) + 3 source rows, 16 columns floor(15 s) + 3).
-constexpr int kMaxRows[4] = {6, 4, 3, 3};
-constexpr int kMaxCols[4] = {10, 6, 4, 3};  // also the staging row pitch
-// tap 0 (stem + layer1) keeps the clip's frame rate: its temporal scale is exactly 1, one frame;
-// taps 1-3 read two frames and stage their temporal blend.
-constexpr int kFrames[4] = {1, 2, 2, 2};
-constexpr int kTapPix[4] = {6 * 10, 4 * 6, 3 * 4, 3 * 3};  // staged pixels (one blended frame)
-constexpr int kPixOff[5] = {0, kTapPix[0], kTapPix[0] + kTapPix[1], kTapPix[0] + kTapPix[1] + kTapPix[2],
-                            kTapPix[0] + kTapPix[1] + kTapPix[2] + kTapPix[3]};
-constexpr int STAGE_FLOATS = kPixOff[4] * PIX;
-// per-thread 16-byte staging elements per tap: ceil(rows * cols * 16 / 256), each kFrames loads
-constexpr int kLoads[4] = {(kTapPix[0] * 16 + 255) / 256, (kTapPix[1] * 16 + 255) / 256, (kTapPix[2] * 16 + 255) / 256,
-                           (kTapPix[3] * 16 + 255) / 256};
-constexpr int kLoadOff[4] = {0, kLoads[0] * kFrames[0], kLoads[0] * kFrames[0] + kLoads[1] * kFrames[1],
-                             kLoads[0] * kFrames[0] + kLoads[1] * kFrames[1] + kLoads[2] * kFrames[2]};
-constexpr int kLoadsTotal = kLoadOff[3] + kLoads[3] * kFrames[3];
-constexpr int kLiveOff[5] = {0, kLoads[0], kLoads[0] + kLoads[1], kLoads[0] + kLoads[1] + kLoads[2],
-                             kLoads[0] + kLoads[1] + kLoads[2] + kLoads[3]};
+constexpr int TILE_W = 16;
+// Tile = TH rows x 16 columns of one frame, TH / 2 waves (2 voxel rows each). Source window bounds
+// per tap (tap i: scale (in-1)/(out-1) < 2^-(i+1), so TH rows touch at most floor((TH-1) s) + 3
+// source rows, 16 columns floor(15 s) + 3).
+template <int TH>
+struct DecGeo {
+  static constexpr int NTHR = 32 * TH;
+  static constexpr int rows(int i) { return ((TH - 1) >> (i + 1)) + 3; }
+  static constexpr int cols(int i) { return (15 >> (i + 1)) + 3; }  // also the staging row pitch
+  static constexpr int kMaxRows[4] = {rows(0), rows(1), rows(2), rows(3)};
+  static constexpr int kMaxCols[4] = {cols(0), cols(1), cols(2), cols(3)};
+  // tap 0 (stem + layer1) keeps the clip's frame rate: its temporal scale is exactly 1, one frame;
+  // taps 1-3 read two frames and stage their temporal blend.
+  static constexpr int kFrames[4] = {1, 2, 2, 2};
+  static constexpr int kTapPix[4] = {rows(0) * cols(0), rows(1) * cols(1), rows(2) * cols(2), rows(3) * cols(3)};
+  static constexpr int kPixOff[5] = {0, kTapPix[0], kTapPix[0] + kTapPix[1], kTapPix[0] + kTapPix[1] + kTapPix[2],
+                                     kTapPix[0] + kTapPix[1] + kTapPix[2] + kTapPix[3]};
+  static constexpr int STAGE_FLOATS = kPixOff[4] * PIX;
+  // per-thread 16-byte staging elements per tap: ceil(rows * cols * 16 / NTHR), each kFrames loads
+  static constexpr int ld(int i) { return (kTapPix[i] * 16 + NTHR - 1) / NTHR; }
+  static constexpr int kLoads[4] = {ld(0), ld(1), ld(2), ld(3)};
+  static constexpr int kLoadOff[4] = {0, ld(0), ld(0) + 2 * ld(1), ld(0) + 2 * ld(1) + 2 * ld(2)};
+  static constexpr int kLoadsTotal = ld(0) + 2 * (ld(1) + ld(2) + ld(3));
+  static constexpr int kLiveOff[5] = {0, ld(0), ld(0) + ld(1), ld(0) + ld(1) + ld(2), ld(0) + ld(1) + ld(2) + ld(3)};
+};
+// the 8 x 16 tile of rounds 1-4: 30 KB of staging, 5 blocks (4 in MODE 4) per CU
+static_assert(DecGeo<8>::STAGE_FLOATS == 105 * PIX && DecGeo<8>::kLoadsTotal == 12, "8-row tile geometry");
 
 struct Win {
   int t0, t1, nf, r0, nr, c0, nc;
@@ -247,11 +254,14 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
 // MODE: 0 = fp32 (v_mfma_f32_16x16x4_f32 comb_2), 1 = bf16 comb_2, 4 = fp32-accurate comb_2 on six
 // split-bf16 products (the fp32 engines' default); timing knock-outs for tools/convbench.hip
 // (CLASFV_KNOCKOUTS builds only; wrong results): 2 = no comb_2 / head MFMAs, 3 = no interpolation.
-template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ? 4 : 5, MODE == 4 ? 4 : 5))) void decoder_kernel(DecParams p) {
+// TROWS: tile rows (8: 4 waves per block; 16: 8 waves, half the blocks and less halo per voxel)
+template <int MODE, int TROWS = 8>
+__global__ __launch_bounds__(32 * TROWS) __attribute__((amdgpu_waves_per_eu(MODE == 4 ? 4 : 5, MODE == 4 ? 4 : 5))) void decoder_kernel(DecParams p) {
+  using G = DecGeo<TROWS>;
+  constexpr int TILE_H = TROWS, NTHR = G::NTHR;
   constexpr int BF = MODE == 1 || MODE == 4;
   extern __shared__ __align__(16) float smem[];
-  float* stage = smem;  // STAGE_FLOATS
+  float* stage = smem;  // G::STAGE_FLOATS
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // voxel-row loops below are scalar branches
@@ -276,7 +286,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ?
     int a, b;
     float la, lb;
     src_index(tp.st, t, tp.T, a, b, la, lb);
-    const bool two = lb > 0.f && b != a && kFrames[i] == 2;  // else the blend below is exactly P[t0]
+    const bool two = lb > 0.f && b != a && G::kFrames[i] == 2;  // else the blend below is exactly P[t0]
     w.t0 = uni(a);
     w.t1 = uni(two ? b : a);
     w.lt0 = unif(two ? la : 1.f);
@@ -287,36 +297,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ?
     const int c0 = min((int)floorf(tp.sw * (float)w0), tp.W - 1);
     const int c1 = min((int)floorf(tp.sw * (float)(w0 + TILE_W - 1)) + 1, tp.W - 1);
     w.r0 = uni(r0);
-    w.nr = uni(min(r1 - r0 + 1, kMaxRows[i]));
+    w.nr = uni(min(r1 - r0 + 1, G::kMaxRows[i]));
     w.c0 = uni(c0);
-    w.nc = uni(min(c1 - c0 + 1, kMaxCols[i]));
+    w.nc = uni(min(c1 - c0 + 1, G::kMaxCols[i]));
     win[i] = w;
   }
   // All staging loads are issued before the first LDS write (fixed per-tap trip counts, predicated),
   // so one block waits for one HBM/L2 latency instead of one per 16-byte chunk.
-  f32x4 buf[kLoadsTotal];
-  bool live[kLiveOff[4]];  // per (tap, k): the staged element exists in the window
+  f32x4 buf[G::kLoadsTotal];
+  bool live[G::kLiveOff[4]];  // per (tap, k): the staged element exists in the window
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const DecTap& tp = p.tap[i];
     const Win& w = win[i];
-    // staged with the constant row pitch kMaxCols[i] (the decode is a division by a constant;
+    // staged with the constant row pitch G::kMaxCols[i] (the decode is a division by a constant;
     // columns past the window's nc are not loaded and never read)
     // 32-bit element offsets (the launcher checks every tap tensor stays below 2^31 floats): the
     // window origin of each source frame is scalar, the per-lane part one multiply per element
     const int base0 = (((n * tp.T + w.t0) * tp.H + w.r0) * tp.W + w.c0) * 64;
     const int base1 = base0 + (w.t1 - w.t0) * tp.H * tp.W * 64;
 #pragma unroll
-    for (int k = 0; k < kLoads[i]; ++k) {
-      const int e = tid + 256 * k;
+    for (int k = 0; k < G::kLoads[i]; ++k) {
+      const int e = tid + NTHR * k;
       const int c4 = e & 15, px = e >> 4;
-      const int rr = px / kMaxCols[i], cc = px - rr * kMaxCols[i];
-      const bool lv = e < kTapPix[i] * 16 && rr < w.nr && cc < w.nc;
-      live[kLiveOff[i] + k] = lv;
+      const int rr = px / G::kMaxCols[i], cc = px - rr * G::kMaxCols[i];
+      const bool lv = e < G::kTapPix[i] * 16 && rr < w.nr && cc < w.nc;
+      live[G::kLiveOff[i] + k] = lv;
       const int lo = (rr * tp.W + cc) * 64 + c4 * 4;
 #pragma unroll
-      for (int f = 0; f < kFrames[i]; ++f) {
-        f32x4& v = buf[kLoadOff[i] + k * kFrames[i] + f];
+      for (int f = 0; f < G::kFrames[i]; ++f) {
+        f32x4& v = buf[G::kLoadOff[i] + k * G::kFrames[i] + f];
         if (lv) v = *reinterpret_cast<const f32x4*>(tp.p + (f ? base1 : base0) + lo);
       }
     }
@@ -324,13 +334,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ?
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const Win& w = win[i];
-    float* dst = stage + kPixOff[i] * PIX;
+    float* dst = stage + G::kPixOff[i] * PIX;
 #pragma unroll
-    for (int k = 0; k < kLoads[i]; ++k) {
-      const int e = tid + 256 * k;
-      if (live[kLiveOff[i] + k]) {
-        f32x4 v = buf[kLoadOff[i] + k * kFrames[i]];
-        if (kFrames[i] == 2) v = v * w.lt0 + buf[kLoadOff[i] + k * kFrames[i] + 1] * w.lt1;
+    for (int k = 0; k < G::kLoads[i]; ++k) {
+      const int e = tid + NTHR * k;
+      if (live[G::kLiveOff[i] + k]) {
+        f32x4 v = buf[G::kLoadOff[i] + k * G::kFrames[i]];
+        if (G::kFrames[i] == 2) v = v * w.lt0 + buf[G::kLoadOff[i] + k * G::kFrames[i] + 1] * w.lt1;
         *reinterpret_cast<f32x4*>(dst + (e >> 4) * PIX + (e & 15) * 4) = v;
       }
     }
@@ -357,7 +367,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ?
   for (int i = 0; i < 4; ++i) {
     if constexpr (MODE == 3) {  // knock-out: one LDS read per channel group instead of the interpolation
 #pragma unroll
-      for (int c = 0; c < 4; ++c) h1[0][c] += *reinterpret_cast<const f32x4*>(stage + kPixOff[i] * PIX + 4 * q + 16 * c + l16 * PIX);
+      for (int c = 0; c < 4; ++c) h1[0][c] += *reinterpret_cast<const f32x4*>(stage + G::kPixOff[i] * PIX + 4 * q + 16 * c + l16 * PIX);
       continue;
     }
     const DecTap& tp = p.tap[i];
@@ -370,7 +380,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ?
     ya0 = uni(ya0), ya1 = uni(ya1), yb0 = uni(yb0), yb1 = uni(yb1);
     la0 = unif(la0), la1 = unif(la1), lb0 = unif(lb0), lb1 = unif(lb1);
     const int nrows = yb1 - ya0 + 1;  // 1..3, wave-uniform
-    const float* fb = stage + kPixOff[i] * PIX + 4 * q + (ya0 - w.r0) * kMaxCols[i] * PIX;
+    const float* fb = stage + G::kPixOff[i] * PIX + 4 * q + (ya0 - w.r0) * G::kMaxCols[i] * PIX;
     const float* c0p = fb + (x0 - w.c0) * PIX;
     const float* c1p = fb + (x1 - w.c0) * PIX;
 #pragma unroll
@@ -383,7 +393,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ?
       const bool ta = k == 0 || ya1 - ya0 == k, tb = yb0 - ya0 == k || yb1 - ya0 == k;
       const float wa = (k == 0 ? la0 : 0.f) + (ya1 - ya0 == k ? la1 : 0.f);
       const float wb = (yb0 - ya0 == k ? lb0 : 0.f) + (yb1 - ya0 == k ? lb1 : 0.f);
-      const int ro = k * kMaxCols[i] * PIX;
+      const int ro = k * G::kMaxCols[i] * PIX;
       f32x4 hx[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c)
@@ -497,20 +507,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 4 ?
 
 }  // namespace
 
-static hipError_t launch_dec(const DecParams& p, hipStream_t s, int mode) {
+static hipError_t launch_dec(const DecParams& p, hipStream_t s, int mode, int th = 8) {
   if (p.tap[0].T != p.T) return hipErrorInvalidValue;  // tap 0 is staged as a single frame
   for (int i = 0; i < 4; ++i)  // the staging loads use 32-bit element offsets
     if ((size_t)p.N * p.tap[i].T * p.tap[i].H * p.tap[i].W * 64 >= ((size_t)1 << 31)) return hipErrorInvalidValue;
-  const size_t nb = (size_t)(p.H / TILE_H) * (p.W / TILE_W) * p.T * p.N;
+  if (p.H % th || p.W % TILE_W) return hipErrorInvalidValue;
+  const size_t nb = (size_t)(p.H / th) * (p.W / TILE_W) * p.T * p.N;
   if (nb >= ((size_t)1 << 31)) return hipErrorInvalidValue;
-  constexpr size_t lds = (size_t)STAGE_FLOATS * 4;
-  static_assert(lds <= 64 * 1024, "default dynamic LDS limit");
-  void (*k)(DecParams) = mode == 1 ? decoder_kernel<1> : mode == 4 ? decoder_kernel<4> : decoder_kernel<0>;
+  static_assert(DecGeo<16>::STAGE_FLOATS * 4 <= 64 * 1024, "default dynamic LDS limit");
+  const size_t lds = (size_t)(th == 16 ? DecGeo<16>::STAGE_FLOATS : DecGeo<8>::STAGE_FLOATS) * 4;
+  void (*k)(DecParams) = nullptr;
+  if (th == 16)
+    k = mode == 1 ? decoder_kernel<1, 16> : mode == 4 ? decoder_kernel<4, 16> : decoder_kernel<0, 16>;
+  else
+    k = mode == 1 ? decoder_kernel<1> : mode == 4 ? decoder_kernel<4> : decoder_kernel<0>;
 #ifdef CLASFV_KNOCKOUTS
-  if (mode == 2) k = decoder_kernel<2>;
-  if (mode == 3) k = decoder_kernel<3>;
+  if (mode == 2) k = th == 16 ? decoder_kernel<2, 16> : decoder_kernel<2>;
+  if (mode == 3) k = th == 16 ? decoder_kernel<3, 16> : decoder_kernel<3>;
 #endif
-  hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(256), lds, s, p);
+  hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(32 * th), lds, s, p);
   return hipGetLastError();
 }
 
@@ -554,8 +569,9 @@ hipError_t launch_decoder(const DecParams& p, hipStream_t s) {
 }
 
 #ifdef CLASFV_KNOCKOUTS
-// tools/convbench.hip: ko 0 = product; 2, 3 = decoder_kernel's knock-out modes
+// tools/convbench.hip: ko 0 = product; 2, 3 = decoder_kernel's knock-out modes; + 16: 16-row tiles
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko) {
-  return launch_dec(p, s, ko == 2 || ko == 3 ? ko : (p.bf16 ? 1 : p.x3 ? 4 : 0));
+  const int m = ko & 15;
+  return launch_dec(p, s, m == 2 || m == 3 ? m : (p.bf16 ? 1 : p.x3 ? 4 : 0), (ko & 16) ? 16 : 8);
 }
 #endif

@@ -426,7 +426,7 @@ constexpr int W4R_WAVES = 12;
 constexpr int W4R_THREADS = 64 * W4R_WAVES;
 constexpr int W4R_DPW = 2;  // DMA instructions per wave per ring stage (wino4_geometry: NI <= 24)
 constexpr int W4R_STAGE = W4R_WAVES * W4R_DPW * 1024;
-constexpr int W4R_NR = 4, W4R_STEP = 2;  // 4 stages, one barrier per 2 chunks
+constexpr int W4R_NR = 4;  // raw ring stages (a barrier every NR / 2 chunks)
 constexpr int W4R_NZ = 3;  // epilogue plane buffers = N tiles per epilogue round
 constexpr int W4R_LDS = W4R_NZ * W4W_ZBUF * 4;  // 163,296 B
 static_assert(W4R_LDS >= W4R_NR * W4R_STAGE + 1024 && W4R_LDS <= 160 * 1024, "ring and planes fit LDS");
@@ -466,13 +466,16 @@ __device__ inline f32x2 bt_row(const f32x2 (&e)[5]) {
   }
 }
 
-// KO (tools/convbench diagnostics, 0 in the product): 4 no epilogue, 128 no output stores, 512 per-block
-// phase stamps (as conv_wino4w's)
-template <int NTN, bool C8, int KO = 0, bool RELU = true>
+// KO (tools/convbench diagnostics, 0 in the product; results wrong otherwise): 1 no transform, 2 no U
+// loads in the loop, 4 no epilogue, 8 no loop DMAs, 16 no chunk barriers, 128 no output stores, 512
+// per-block phase stamps (as conv_wino4w's). NR: raw ring stages (4: a barrier every 2 chunks; 6: every 3)
+template <int NTN, bool C8, int KO = 0, bool RELU = true, int NR = W4R_NR>
 __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_wino4r(ConvParams p,
                                                                                                        W4Geo g) {
   using WR = W4R<NTN>;
-  constexpr int NR = W4R_NR, STAGE = W4R_STAGE, UQ = WR::UQ, NU = WR::NU, NV = WR::NV;
+  constexpr int STAGE = W4R_STAGE, UQ = WR::UQ, NU = WR::NU, NV = WR::NV;
+  constexpr int STEP = NR / 2;  // chunks per barrier: raw(k) .. raw(k + STEP - 1) land STEP chunks ahead
+  static_assert(NR * STAGE + 1024 <= W4R_LDS, "ring fits the plane buffers' LDS");
   __shared__ __align__(16) char smem[W4R_LDS];
   char* sink = smem + NR * STAGE;
 
@@ -589,10 +592,11 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
   f32x4 u[UQ];
   f32x2 a[3];
 
-  issue_raw(0, 0);
-  __builtin_amdgcn_sched_barrier(0);
-  issue_raw(1, 1);
-  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int d = 0; d < STEP; ++d) {
+    issue_raw(d, d);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 #pragma unroll
   for (int gi = 0; gi < UQ; ++gi) u[gi] = load_u(0, gi);
   __builtin_amdgcn_sched_barrier(0);
@@ -604,7 +608,7 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
 #pragma unroll 1
   do {
     const int ph = k % NR;
-    if (ph % W4R_STEP == 0) {
+    if (ph % STEP == 0) {
       __builtin_amdgcn_s_waitcnt(vm_wait(UQ));
       __builtin_amdgcn_sched_barrier(0);
       if constexpr ((KO & 16) == 0) __builtin_amdgcn_s_barrier();
@@ -615,7 +619,7 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
 #endif
       if constexpr ((KO & 8) == 0) {
 #pragma unroll
-        for (int d = 2; d < NR; ++d) issue_raw(k + d, (ph + d) % NR);
+        for (int d = NR - STEP; d < NR; ++d) issue_raw(k + d, (ph + d) % NR);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -775,17 +779,17 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
 #endif
 }
 
-template <int NTN, int KO = 0>
+template <int NTN, int KO = 0, int NR = W4R_NR>
 hipError_t launch_w4r(const ConvParams& p, const W4Geo& g, int n_blocks, hipStream_t s) {
   const dim3 grid(n_blocks), block(W4R_THREADS);
   if (p.y_c8 && p.relu)
-    hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, true>), grid, block, 0, s, p, g);
+    hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, true, NR>), grid, block, 0, s, p, g);
   else if (p.relu)
-    hipLaunchKernelGGL((conv_wino4r<NTN, false, KO, true>), grid, block, 0, s, p, g);
+    hipLaunchKernelGGL((conv_wino4r<NTN, false, KO, true, NR>), grid, block, 0, s, p, g);
   else if (p.y_c8)
-    hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, false>), grid, block, 0, s, p, g);
+    hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, false, NR>), grid, block, 0, s, p, g);
   else
-    hipLaunchKernelGGL((conv_wino4r<NTN, false, KO, false>), grid, block, 0, s, p, g);
+    hipLaunchKernelGGL((conv_wino4r<NTN, false, KO, false, NR>), grid, block, 0, s, p, g);
   return hipGetLastError();
 }
 
@@ -975,7 +979,7 @@ hipError_t launch_wino4w_ko(const ConvParams& p, hipStream_t s, int ko) {
     default: return launch_w4w_dpw<9>(p, g, nb, s);
   }
 }
-// tools/convbench: conv_wino4r diagnostics (KO bits 4, 128, 512 of conv_wino4r), NTN = 9 only
+// tools/convbench: conv_wino4r diagnostics (KO bits of conv_wino4r; 64: the 6-stage ring), NTN = 9 only
 hipError_t launch_wino4r_ko(const ConvParams& p, hipStream_t s, int ko) {
   if (!wino4w_supported(p) || wino4w_ntn(p.Cout) != 9) return hipErrorInvalidValue;
   W4Geo g;
@@ -990,6 +994,8 @@ hipError_t launch_wino4r_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 4: return launch_w4r<9, 4>(p, g, nb, s);
     case 128: return launch_w4r<9, 128>(p, g, nb, s);
     case 512: return launch_w4r<9, 512>(p, g, nb, s);
+    case 64: return launch_w4r<9, 0, 6>(p, g, nb, s);     // 6-stage ring, a barrier every 3 chunks
+    case 576: return launch_w4r<9, 512, 6>(p, g, nb, s);  // the same with stamps
     default: return launch_w4r<9>(p, g, nb, s);
   }
 }
