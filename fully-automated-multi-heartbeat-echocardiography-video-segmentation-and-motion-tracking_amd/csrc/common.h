@@ -94,6 +94,7 @@ struct DecParams {
   int N, T, H, W;
   int bf16;           // comb_2 on bf16 MFMAs (bf16 engines; taps, heads and outputs stay fp32)
   int x3;             // fp32 engines: comb_2 as six bf16 products of 3-way split operands (fp32-accurate)
+  int rows16;         // CLASFV_VARIANT_DECODER_ROWS16: the X3 decoder on 16-row tiles instead of 8
 };
 
 // Launchers (stream-ordered, no synchronisation). Return hipError_t of the launch.
@@ -126,7 +127,9 @@ double wino4w_exec_gflop(const ConvParams& p);
 void wino4w_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 size_t wino4w_weight_floats(int cin_p, int cout_p);  // 0: no wide block for this cout_p
 // conv_wino4r: conv_wino4w's arithmetic on 12 row waves per block (3 per SIMD), its own U layout
+bool wino4r_supported(const ConvParams& p);
 hipError_t launch_wino4r(const ConvParams& p, hipStream_t s);
+double wino4r_exec_gflop(const ConvParams& p);
 void wino4r_transform_weights(const double* w, int cout, int cin, int cout_p, int cin_p, float* U);
 size_t wino4r_weight_floats(int cin_p, int cout_p);
 // Fused Winograd F(4,3)-in-time path for stride-1 3x1x1 fp32 convs; p.w = transformed weights.

@@ -124,6 +124,7 @@ int env_variants() {
   if (on("CLASFV_NO_PATCH32")) f |= CLASFV_VARIANT_NO_PATCH32;
   if (on("CLASFV_NO_PROJ_X3")) f |= CLASFV_VARIANT_NO_PROJ_X3;
   if (on("CLASFV_NO_WINO4R")) f |= CLASFV_VARIANT_NO_WINO4R;
+  if (on("CLASFV_DECODER_ROWS16")) f |= CLASFV_VARIANT_DECODER_ROWS16;
   return f;
 }
 
@@ -351,7 +352,7 @@ double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
     ConvParams p{};                                                           // tile and channel pair, 16-tile groups
     p.N = out.n, p.Ti = p.To = out.t, p.Hi = p.Ho = out.h, p.Wi = p.Wo = out.w;
     p.Cin = c.cin_p, p.Cout = c.cout_p;
-    return kname[10] ? wino4w_exec_gflop(p) : wino4_exec_gflop(p);  // conv_wino4r: conv_wino4w's groups
+    return kname[10] == 'r' ? wino4r_exec_gflop(p) : kname[10] == 'w' ? wino4w_exec_gflop(p) : wino4_exec_gflop(p);
   }
   if (!strcmp(kname, "conv_wino_q") || !strcmp(kname, "conv_wino"))
     return 2.0 * nt * ((out.h + 1) / 2) * ((out.w + 1) / 2) * 16.0 * cc * 1e-9;
@@ -410,8 +411,9 @@ const char* pick_kernel(const Conv& c, ConvParams p) {
   // (convbench 0.284 vs 0.312 ms per 1152-channel launch, profiles/r03p_dma_x3_tiles.txt); per-clip
   // shape rule
   if (c.dwino4 && c.dx3 && p.Ho * p.Wo <= 64 && !p.y_c8 && dma_x3_supported(p)) return "conv_dma_x3";
-  if (c.dwino4w && !(p.vflags & (CLASFV_VARIANT_NO_WINO4 | CLASFV_VARIANT_NO_WINO4W)) && wino4w_supported(p))
-    return c.dwino4r && !(p.vflags & CLASFV_VARIANT_NO_WINO4R) ? "conv_wino4r" : "conv_wino4w";
+  const int no4 = p.vflags & (CLASFV_VARIANT_NO_WINO4 | CLASFV_VARIANT_NO_WINO4W);
+  if (c.dwino4r && !no4 && !(p.vflags & CLASFV_VARIANT_NO_WINO4R) && wino4r_supported(p)) return "conv_wino4r";
+  if (c.dwino4w && !no4 && wino4w_supported(p)) return "conv_wino4w";
   if (c.dwino4 && !(p.vflags & CLASFV_VARIANT_NO_WINO4) && wino4_supported(p)) return "conv_wino4";
   if (c.dwino) {
     const bool no_patch = (p.vflags & CLASFV_VARIANT_NO_WINO_PATCH) != 0;
@@ -750,6 +752,8 @@ int clasfv_finalize(clasfv_t h) {
         std::vector<float> uw(wino4w_weight_floats(c.cin_p, c.cout_p));
         wino4w_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, uw.data());
         if ((rc = upload(uw, &c.dwino4w))) return rc;
+      }
+      if (c.cin_p % 8 == 0 && wino4r_weight_floats(c.cin_p, c.cout_p)) {
         std::vector<float> ur(wino4r_weight_floats(c.cin_p, c.cout_p));
         wino4r_transform_weights(wf.data(), c.cout, cin, c.cout_p, c.cin_p, ur.data());
         if ((rc = upload(ur, &c.dwino4r))) return rc;
@@ -888,7 +892,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0x1FFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~0x3FFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;
@@ -1057,6 +1061,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   d.bf16 = h->dtype == CLASFV_DTYPE_BF16 && !(h->tune.vflags & CLASFV_VARIANT_NO_DECODER_BF16);
   d.w2x3 = h->w2x3;
   d.x3 = h->dtype != CLASFV_DTYPE_BF16 && !(h->tune.vflags & CLASFV_VARIANT_NO_DECODER_X3);
+  d.rows16 = (h->tune.vflags & CLASFV_VARIANT_DECODER_ROWS16) != 0;
   HIP_TRY(launch_decoder(d, s));
   // comb_2 (64x64) and the heads (6 useful of the 16 rows of their MFMA tile) per output voxel, in the
   // products of the pipe they run on: fp32 engines six split-bf16 products each (bf16 pipe), bf16

@@ -436,7 +436,7 @@ static_assert(W4R_LDS >= W4R_NR * W4R_STAGE + 1024 && W4R_LDS <= 160 * 1024, "ri
 template <int NTN>
 struct W4R {
   static constexpr int NV = 6 * NTN;
-  static constexpr int UQ = NTN == 9 ? 7 : 9;
+  static constexpr int UQ = NTN == 9 ? 7 : NTN == 5 ? 8 : 9;
   static constexpr int NU = (NV + 4 * UQ - 1) / (4 * UQ) * UQ;
 };
 
@@ -469,7 +469,7 @@ __device__ inline f32x2 bt_row(const f32x2 (&e)[5]) {
 // KO (tools/convbench diagnostics, 0 in the product; results wrong otherwise): 1 no transform, 2 no U
 // loads in the loop, 4 no epilogue, 8 no loop DMAs, 16 no chunk barriers, 128 no output stores, 512
 // per-block phase stamps (as conv_wino4w's). NR: raw ring stages (4: a barrier every 2 chunks; 6: every 3)
-template <int NTN, bool C8, int KO = 0, bool RELU = true, int NR = W4R_NR>
+template <int NTN, bool C8, int KO = 0, bool RELU = true, int NR = W4R_NR, int CPB = 1>
 __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_wino4r(ConvParams p,
                                                                                                        W4Geo g) {
   using WR = W4R<NTN>;
@@ -550,9 +550,9 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
 #pragma unroll
         for (int q = 0; q < 5; ++q) e[q] = *reinterpret_cast<const f32x2*>(base + q * rp16 + co);
         tt[c] = bt_row<RH, RR>(e);
-        // one column's window reads in flight at a time: 168 registers hold 108 accumulators and the
+        // CPB columns' window reads in flight at a time: 168 registers hold 108 accumulators and the
         // U ring (hoisting every column's reads spilled)
-        __builtin_amdgcn_sched_barrier(0);
+        if (c % CPB == CPB - 1) __builtin_amdgcn_sched_barrier(0);
       }
       bt_cols<CH>(tt, a);
     };
@@ -779,17 +779,17 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
 #endif
 }
 
-template <int NTN, int KO = 0, int NR = W4R_NR>
+template <int NTN, int KO = 0, int NR = W4R_NR, int CPB = 1>
 hipError_t launch_w4r(const ConvParams& p, const W4Geo& g, int n_blocks, hipStream_t s) {
   const dim3 grid(n_blocks), block(W4R_THREADS);
   if (p.y_c8 && p.relu)
-    hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, true, NR>), grid, block, 0, s, p, g);
+    hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, true, NR, CPB>), grid, block, 0, s, p, g);
   else if (p.relu)
-    hipLaunchKernelGGL((conv_wino4r<NTN, false, KO, true, NR>), grid, block, 0, s, p, g);
+    hipLaunchKernelGGL((conv_wino4r<NTN, false, KO, true, NR, CPB>), grid, block, 0, s, p, g);
   else if (p.y_c8)
-    hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, false, NR>), grid, block, 0, s, p, g);
+    hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, false, NR, CPB>), grid, block, 0, s, p, g);
   else
-    hipLaunchKernelGGL((conv_wino4r<NTN, false, KO, false, NR>), grid, block, 0, s, p, g);
+    hipLaunchKernelGGL((conv_wino4r<NTN, false, KO, false, NR, CPB>), grid, block, 0, s, p, g);
   return hipGetLastError();
 }
 
@@ -903,21 +903,50 @@ void wino4w_transform_weights(const double* w, int cout, int cin, int cout_p, in
     }
 }
 
-// conv_wino4r (12 row waves per block) on conv_wino4w's tile groups; p.w: wino4r_transform_weights' layout.
-hipError_t launch_wino4r(const ConvParams& p, hipStream_t s) {
-  if (!wino4w_supported(p)) return hipErrorInvalidValue;
+// NTN of conv_wino4r for a Cout: the widest of 9, 6 N tiles dividing it (0: none). NTN = 5 (layer2's
+// 240-channel conv) compiles (W4R<5>) but ran 0.747 vs conv_wino4's 0.723 ms
+// (profiles/r05o_wino4r_ntn5.txt): conv_wino4 keeps that conv.
+int wino4r_ntn(int cout) {
+  if (cout % 16) return 0;
+  for (int n : {9, 6})
+    if ((cout / 16) % n == 0) return n;
+  return 0;
+}
+
+static int w4r_nu(int ntn) { return ntn == 9 ? W4R<9>::NU : ntn == 6 ? W4R<6>::NU : W4R<5>::NU; }
+
+bool wino4r_supported(const ConvParams& p) {
   W4Geo g;
   int nb;
-  const int ntn = wino4w_ntn(p.Cout);
+  const int ntn = wino4r_ntn(p.Cout);
+  return ntn && !p.in_bf16 && !p.out_bf16 && !p.stem && !p.x2 && !p.res && p.KT == 1 && p.KH == 3 && p.KW == 3 &&
+         p.sh == 1 && p.sw == 1 && p.st == 1 && p.ph == 1 && p.pw == 1 && p.pt == 0 && p.Ho == p.Hi &&
+         p.Wo == p.Wi && p.To == p.Ti &&
+         (size_t)p.N * p.To * p.Ho * p.Wo * (p.Cin > p.Cout ? p.Cin : p.Cout) < ((size_t)1 << 31) &&
+         wino4_geometry(p, &g, &nb, 16 * ntn, W4W_FILL);
+}
+
+// conv_wino4r (12 row waves per block) on conv_wino4w's tile groups; p.w: wino4r_transform_weights' layout.
+hipError_t launch_wino4r(const ConvParams& p, hipStream_t s) {
+  if (!wino4r_supported(p)) return hipErrorInvalidValue;
+  W4Geo g;
+  int nb;
+  const int ntn = wino4r_ntn(p.Cout);
   wino4_geometry(p, &g, &nb, 16 * ntn, W4W_FILL);
   return ntn == 9 ? launch_w4r<9>(p, g, nb, s) : launch_w4r<6>(p, g, nb, s);
 }
 
+double wino4r_exec_gflop(const ConvParams& p) {
+  W4Geo g;
+  int nb;
+  const int ntn = wino4r_ntn(p.Cout);
+  return ntn && wino4_geometry(p, &g, &nb, 16 * ntn, W4W_FILL) ? 2.0 * nb * 16.0 * 36.0 * p.Cin * 16.0 * ntn * 1e-9 : 0.0;
+}
+
 size_t wino4r_weight_floats(int cin_p, int cout_p) {
-  const int ntn = wino4w_ntn(cout_p);
+  const int ntn = wino4r_ntn(cout_p);
   if (!ntn) return 0;
-  const int nu = ntn == 9 ? W4R<9>::NU : W4R<6>::NU;
-  return (size_t)(cout_p / (16 * ntn)) * (cin_p / 8) * W4R_WAVES * nu * 256;
+  return (size_t)(cout_p / (16 * ntn)) * (cin_p / 8) * W4R_WAVES * w4r_nu(ntn) * 256;
 }
 
 // U[cout_p/(16 NTN)][cin_p/8][12 waves][NU][64 lane][4]: wave (rh, ch, r) = (w / 6, (w / 3) % 2, w % 3),
@@ -931,8 +960,8 @@ void wino4r_transform_weights(const double* w, int cout, int cin, int cout_p, in
                                  {1.0 / 24, 1.0 / 12, 1.0 / 6},
                                  {1.0 / 24, -1.0 / 12, 1.0 / 6},
                                  {0, 0, 1}};
-  const int ntn = wino4w_ntn(cout_p);
-  const int nu = ntn == 9 ? W4R<9>::NU : W4R<6>::NU;
+  const int ntn = wino4r_ntn(cout_p);
+  const int nu = w4r_nu(ntn);
   const int nch = cin_p / 8, cw = 16 * ntn;
   const size_t total = wino4r_weight_floats(cin_p, cout_p);
   for (size_t i = 0; i < total; ++i) U[i] = 0.f;
@@ -995,6 +1024,8 @@ hipError_t launch_wino4r_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 128: return launch_w4r<9, 128>(p, g, nb, s);
     case 512: return launch_w4r<9, 512>(p, g, nb, s);
     case 64: return launch_w4r<9, 0, 6>(p, g, nb, s);     // 6-stage ring, a barrier every 3 chunks
+    case 32: return launch_w4r<9, 0, 4, 2>(p, g, nb, s);  // 2 window columns' LDS reads in flight
+    case 96: return launch_w4r<9, 0, 4, 3>(p, g, nb, s);  // 3
     case 576: return launch_w4r<9, 512, 6>(p, g, nb, s);  // the same with stamps
     default: return launch_w4r<9>(p, g, nb, s);
   }

@@ -399,30 +399,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // B^T row e of tile m, formed right before its MFMAs (the 12 transformed values of both tiles
     // held at once, beside the 192-register accumulator, spilled at NT = 4); the same expressions
     // as the reference kernel, per element
-    // Both channels of the lane's pair at once on packed f32 VALU (v_pk_mul / v_pk_add / v_pk_fma),
-    // with the roundings of the scalar expressions as hipcc compiles them in conv_winot (rows 0 and
-    // 5: two products, a difference, a sum; rows 1-4: one fused multiply-add), so the two kernels stay
-    // bit-identical; the per-channel scalar form cost ~60 VALU + ~35 register moves per chunk.
     auto vrow = [&](int m, int e) __attribute__((always_inline)) {
-#pragma clang fp contract(off)
-      if constexpr ((EPI & 256) != 0) return d[MS * m + e];
-      const f32x2 d0 = d[MS * m], d1 = d[MS * m + 1], d2 = d[MS * m + 2], d3 = d[MS * m + 3], d4 = d[MS * m + 4],
-                  d5 = d[MS * m + 5];
-      if (e == 0) {
-        const f32x2 a = d0 * 4.f, b = d2 * 5.f;
-        return (a - b) + d4;
-      } else if (e == 1) {
-        return __builtin_elementwise_fma(f32x2{-4.f, -4.f}, d1 + d2, d3 + d4);
-      } else if (e == 2) {
-        return __builtin_elementwise_fma(f32x2{4.f, 4.f}, d1 - d2, d4 - d3);
-      } else if (e == 3) {
-        return __builtin_elementwise_fma(f32x2{2.f, 2.f}, d3 - d1, d4 - d2);
-      } else if (e == 4) {
-        return __builtin_elementwise_fma(f32x2{-2.f, -2.f}, d3 - d1, d4 - d2);
+      f32x2 r;
+      if constexpr ((EPI & 256) != 0) {
+        r = d[MS * m + e];
       } else {
-        const f32x2 a = d1 * 4.f, b = d3 * 5.f;
-        return (a - b) + d5;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const float d0 = d[MS * m][s2], d1 = d[MS * m + 1][s2], d2 = d[MS * m + 2][s2], d3 = d[MS * m + 3][s2],
+                      d4 = d[MS * m + 4][s2], d5 = d[MS * m + 5][s2];
+          float x;
+          if (e == 0) x = 4.f * d0 - 5.f * d2 + d4;
+          else if (e == 1) { const float e1 = d3 + d4, e2 = d1 + d2; x = e1 - 4.f * e2; }
+          else if (e == 2) { const float e3 = d4 - d3, e4 = d1 - d2; x = e3 + 4.f * e4; }
+          else if (e == 3) x = (d4 - d2) + 2.f * (d3 - d1);
+          else if (e == 4) x = (d4 - d2) - 2.f * (d3 - d1);
+          else x = 4.f * d1 - 5.f * d3 + d5;
+          r[s2] = x;
+        }
       }
+      return r;
     };
 #pragma unroll
     for (int e = 0; e < 6; ++e) {

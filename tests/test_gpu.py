@@ -700,6 +700,21 @@ def test_decoder_x3_matches_fp32_mfma(model, shape):
     np.testing.assert_allclose(m3.cpu().numpy(), m1.cpu().numpy(), rtol=0, atol=MOT_ATOL / 4)
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (3, 3, 8, 32, 48)])
+def test_decoder_16row_tiles_bitexact(model, shape):
+    """The fp32 engines' decoder on 16 x 16-voxel tiles (8 waves per block; variant decoder_rows16,
+    round 5) against the product's 8 x 16 tiles (csrc/decoder.hip DecGeo): every voxel's staging blend,
+    interpolation, comb_2 and heads are the same expressions in the same order, so the seg logits and
+    motion are bit-identical; only the block shape (and the staged halo per voxel) changes."""
+    rng = np.random.default_rng(61)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    s8, m8 = model(x)
+    model.set_kernel_variants("decoder_rows16")
+    s16, m16 = model(x)
+    model.set_kernel_variants()
+    assert torch.equal(s16, s8) and torch.equal(m16, m8)
+
+
 @pytest.mark.parametrize("variant", ["no_dma_x3", "no_stem_x3"])
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (3, 3, 8, 32, 48)])
 def test_x3_convs_match_fp32_mfma(model, shape, variant):

@@ -126,12 +126,14 @@ int main(int argc, char** argv) {
   const size_t nx = (size_t)N * T * H * W * Cin, ny = (size_t)p.M * Cout;
   p.x = bf ? to_bf16_dev(nx, 0.f, 1.f, 1) : dev_random(nx, 0.f, 1.f, 1);
   const size_t nw = wino4w ? wino4w_weight_floats(Cin, Cout) : wino4 ? (size_t)(Cout / 48) * (Cin / 8) * 14336 : winor ? (size_t)24 * Cin * Cout : wino ? (size_t)16 * Cin * Cout : winot ? (size_t)6 * Cin * Cout : (size_t)Cout * p.Kp;
-  p.w = bf ? to_bf16_dev(nw, -0.05f, 0.05f, 2) : dev_random(nw, -0.05f, 0.05f, 2);
+  p.w = bf ? to_bf16_dev(nw, -0.05f, 0.05f, 2) : dev_random(nw ? nw : 1, -0.05f, 0.05f, 2);
   p.bias = (const float*)dev_random(Cout, -0.1f, 0.1f, 3);
   p.res = (getenv("CB_NORES") || wino4 || wino4w) ? nullptr : bf ? to_bf16_dev(ny, 0.f, 1.f, 4) : dev_random(ny, 0.f, 1.f, 4);
   CK(hipMalloc(&p.y, ny * 4));
   void* w4r = nullptr;
-  if (wino4r) {
+  if (wino4r && !nw) {  // no conv_wino4w form for this Cout (NTN = 5): a random wino4r image
+    w4r = dev_random(wino4r_weight_floats(Cin, Cout), -0.05f, 0.05f, 2);
+  } else if (wino4r) {
     std::vector<float> uw(nw), urr(wino4r_weight_floats(Cin, Cout));
     CK(hipMemcpy(uw.data(), p.w, nw * 4, hipMemcpyDeviceToHost));
     wino4r_from_wino4w(uw.data(), Cin, Cout, urr.data());
