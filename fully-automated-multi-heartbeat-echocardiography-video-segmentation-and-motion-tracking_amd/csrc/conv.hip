@@ -368,7 +368,17 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
 // operands from its f32x4 slot of each step -- the same k set on both sides of the product.
 // WN: waves along N (1: 4 waves x (BM/4 rows x BN); 2: 2 x 2 waves of (BM/2 rows x BN/2), halving the
 // B-piece LDS reads per wave at twice the A splits).
-template <int MT, int NT, int S, int WN = 1, int EF = -1>
+// BUF (round 5; dma_x3_buf_ok: every tensor below 2^31 bytes, <= 31 taps): the DMAs as buffer loads
+// with 32-bit offsets. A row's tap validity is a bit mask computed once per block and its pixel
+// offset a per-row constant, so an A DMA costs 3 VALU (bit test, select of the row offset or an
+// out-of-range offset, whose DMA reads zeros) beside a scalar tap / channel offset, and a B DMA
+// none; the pointer form spent ~14 VALU per A DMA (bounds compares, 64-bit address, select) in a
+// kernel whose split VALU already competes with the MFMAs for issue (profiles/r05q_dma_x3_knockouts.txt:
+// no loop DMAs -25 % on layer2's 240-channel strided conv).
+// KO (tools/convbench timing knock-outs, 0 in the product; results wrong otherwise): 1 no activation
+// split (the fp32 bits reinterpreted as the three pieces), 2 no B-piece LDS reads, 4 no DMAs in the
+// loop, 8 no waits / barriers, 16 no epilogue.
+template <int MT, int NT, int S, int WN = 1, int EF = -1, int KO = 0, bool BUF = false>
 __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, DmaDivs dv) {
   static_assert(NT % WN == 0, "N tiles split evenly over the waves along N");
   constexpr int MTW = MT * WN, NTW = NT / WN;  // 16 x 16 tiles per wave
@@ -417,11 +427,44 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
     d_pix[j] = ((mt * p.Ti + d_t[j]) * p.Hi + d_h[j]) * p.Wi + d_w[j];
   }
   const __bf16* d_wrow[B_PER];
+  unsigned b_bo[B_PER];  // BUF: byte offsets into the weight image
 #pragma unroll
   for (int j = 0; j < B_PER; ++j) {
     const int idx = wid + 4 * j;  // B instruction: piece idx / NT, rows 16 (idx % NT) ..
     const int pc = idx / NT, nr = idx - pc * NT;
-    d_wrow[j] = idx < B_INS ? w + ((size_t)(n0 + nr * 16 + drow) * npairs * 3 + pc) * 32 + 8 * dq : w;
+    if constexpr (BUF)
+      b_bo[j] = idx < B_INS ? (unsigned)(((n0 + nr * 16 + drow) * npairs * 3 + pc) * 64 + 16 * dq) : 0u;
+    else
+      d_wrow[j] = idx < B_INS ? w + ((size_t)(n0 + nr * 16 + drow) * npairs * 3 + pc) * 32 + 8 * dq : w;
+  }
+  // BUF: per A row, the tap-validity bits (tap = (kt KH + kh) KW + kw; 0 for a row past M) and the
+  // byte offsets of its first tap's pixel in x and x2 (16-B slot dq included)
+  unsigned a_vm[A_PER], a_bo[A_PER], a_bo2[A_PER];
+  const int padpix = (p.pt * p.Hi + p.ph) * p.Wi + p.pw;  // the most negative first-tap pixel of a row
+  const size_t vox = (size_t)p.N * p.Ti * p.Hi * p.Wi;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      BUF ? const_cast<float*>(x - (size_t)padpix * p.Cin) : nullptr, (short)0,
+      BUF ? (int)((vox + padpix) * p.Cin * 4) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x2r = __builtin_amdgcn_make_buffer_rsrc(
+      BUF && x2 ? const_cast<float*>(x2) : nullptr, (short)0, BUF && x2 ? (int)(vox * p.Cin2 * 4) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      BUF ? const_cast<__bf16*>(w) : nullptr, (short)0, BUF ? (int)((size_t)n_tiles * BN * npairs * 192) : 0, 0x00020000);
+  if constexpr (BUF) {
+#pragma unroll
+    for (int j = 0; j < A_PER; ++j) {
+      unsigned vm = 0;
+      for (int kt = 0; kt < p.KT; ++kt)
+        for (int kh = 0; kh < p.KH; ++kh)
+          for (int kw = 0; kw < p.KW; ++kw) {
+            const int ti = d_t[j] + kt, hi = d_h[j] + kh, wi = d_w[j] + kw;
+            const bool ok = ((unsigned)ti < (unsigned)p.Ti) & ((unsigned)hi < (unsigned)p.Hi) & ((unsigned)wi < (unsigned)p.Wi);
+            vm |= (ok ? 1u : 0u) << ((kt * p.KH + kh) * p.KW + kw);
+          }
+      a_vm[j] = vm;
+      // offsets from x - padpix pixels: never negative for a valid tap, so neither buffer offset wraps
+      a_bo[j] = (unsigned)(d_pix[j] + padpix) * (unsigned)(p.Cin * 4) + 16u * (unsigned)dq;
+      a_bo2[j] = (unsigned)d_pix[j] * (unsigned)(p.Cin2 * 4) + 16u * (unsigned)dq;
+    }
   }
   const int khw = p.KH * p.KW;
   const int kmain = p.KT * khw * p.Cin;
@@ -466,6 +509,19 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
           c_tap_pix = (c_kt * p.Hi + c_kh) * p.Wi + c_kw;
         }
       }
+      if constexpr (BUF) {
+        // tap 31: no row's bit (<= 31 taps), the padding step of an odd K reads zeros
+        const unsigned tap = valid ? (unsigned)((kt * p.KH + kh) * p.KW + kw) : 31u;
+        const unsigned soff = (unsigned)(tap_pix * cin + c0) * 4u;
+#pragma unroll
+        for (int j = 0; j < A_PER; ++j) {
+          const unsigned off = ((a_vm[j] >> tap) & 1u) ? (second ? a_bo2[j] : a_bo[j]) : 0x80000000u;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              second ? x2r : xr, (__attribute__((address_space(3))) void*)(stg + sub * A_BYTES + (wid * A_PER + j) * 1024),
+              16, off, soff, 0, 0);
+        }
+        continue;
+      }
       const float* xc = xb + c0 + 4 * dq;
 #pragma unroll
       for (int j = 0; j < A_PER; ++j) {
@@ -483,10 +539,17 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
 #pragma unroll
     for (int j = 0; j < B_PER; ++j) {
       const int idx = wid + 4 * j;
-      const void* src = idx < B_INS ? (const void*)(d_wrow[j] + (size_t)pair * 96) : p.zero;
       char* dst = idx < B_INS ? stg + 2 * A_BYTES + idx * 1024 : smem + JUNK;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      if constexpr (BUF) {
+        // (offsets through locals: a captured array element as the builtin's operand made the host-side
+        // instantiation fail substitution)
+        const unsigned bo = b_bo[j], so = (unsigned)pair * 192u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)dst, 16, bo, so, 0, 0);
+      } else {
+        const void* src = idx < B_INS ? (const void*)(d_wrow[j] + (size_t)pair * 96) : p.zero;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      }
     }
   };
 
@@ -506,29 +569,43 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
   const int a_off = (wm * 16 * MTW + l16) * 64 + pq * 16;
   const int b_off = 2 * A_BYTES + (wn * NTW) * 1024 + l16 * 64 + pq * 16;
   for (int k = 0; k < nk; ++k) {
-    if (k + S - 2 < nk) {
-      if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 * PER_WAVE) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr ((KO & 8) == 0) {
+      if (k + S - 2 < nk) {
+        if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 * PER_WAVE) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (k + S - 1 < nk) issue(kb + k + S - 1, (k + S - 1) % S);
+    if constexpr ((KO & 4) == 0)
+      if (k + S - 1 < nk) issue(kb + k + S - 1, (k + S - 1) % S);
     const char* st = smem + (k % S) * STAGE;
     bf16x8 ah[MTW], am[MTW], al[MTW];
 #pragma unroll
     for (int i = 0; i < MTW; ++i) {
       const f32x4 a0 = *reinterpret_cast<const f32x4*>(st + a_off + i * 16 * 64);
       const f32x4 a1 = *reinterpret_cast<const f32x4*>(st + A_BYTES + a_off + i * 16 * 64);
-      split3_bf16x8(a0, a1, ah[i], am[i], al[i]);
+      if constexpr ((KO & 1) != 0) {
+        ah[i] = __builtin_bit_cast(bf16x8, a0);
+        am[i] = __builtin_bit_cast(bf16x8, a1);
+        al[i] = ah[i];
+      } else {
+        split3_bf16x8(a0, a1, ah[i], am[i], al[i]);
+      }
     }
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
-      const bf16x8 bh = *reinterpret_cast<const bf16x8*>(st + b_off + j * 1024);
-      const bf16x8 bm = *reinterpret_cast<const bf16x8*>(st + b_off + (NT + j) * 1024);
-      const bf16x8 bl = *reinterpret_cast<const bf16x8*>(st + b_off + (2 * NT + j) * 1024);
+      bf16x8 bh, bm, bl;
+      if constexpr ((KO & 2) != 0) {
+        bh = ah[0], bm = am[0], bl = al[0];
+      } else {
+        bh = *reinterpret_cast<const bf16x8*>(st + b_off + j * 1024);
+        bm = *reinterpret_cast<const bf16x8*>(st + b_off + (NT + j) * 1024);
+        bl = *reinterpret_cast<const bf16x8*>(st + b_off + (2 * NT + j) * 1024);
+      }
 #pragma unroll
       for (int i = 0; i < MTW; ++i) {
         f32x4 c = acc[i][j];
@@ -540,6 +617,15 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah[i], c, 0, 0, 0);
       }
     }
+  }
+  if constexpr ((KO & 16) != 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) sum += acc[i][j][0] + acc[i][j][3];
+    if (sum == 1234.5f) reinterpret_cast<float*>(p.y)[tid] = sum;
+    return;
   }
   if (n_split > 1)
     partial_store<MTW, NTW>(p, acc, p.part + (size_t)split * p.M * p.Cout, m0 + wm * 16 * MTW, n0 + wn * 16 * NTW, q,
@@ -898,6 +984,19 @@ hipError_t launch_dma(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// conv_dma_x3's buffer-offset DMAs (BUF): every byte offset they form stays below 2^31 (the input
+// from padpix pixels before its start, the second input, the weight image of rows_alloc rows) and
+// the tap mask fits 31 bits (CLASFV_VARIANT_NO_DMA_BUF: the pointer form everywhere)
+bool dma_x3_buf_ok(const ConvParams& p, int rows_alloc) {
+  if (p.vflags & CLASFV_VARIANT_NO_DMA_BUF) return false;
+  const size_t lim = (size_t)1 << 31;
+  const size_t vox = (size_t)p.N * p.Ti * p.Hi * p.Wi;
+  const size_t padpix = ((size_t)p.pt * p.Hi + p.ph) * p.Wi + p.pw;
+  const int npairs = (p.Kp / 16 + 1) / 2;
+  return p.KT * p.KH * p.KW <= 31 && (vox + padpix) * p.Cin * 4 < lim && (!p.x2 || vox * p.Cin2 * 4 < lim) &&
+         (size_t)rows_alloc * npairs * 192 < lim;
+}
+
 template <int MT, int NT, int S, int WN = 1>
 hipError_t launch_dma_x3_t(const ConvParams& p, hipStream_t s) {
   constexpr int BM = 64 * MT, BN = 16 * NT;
@@ -905,13 +1004,25 @@ hipError_t launch_dma_x3_t(const ConvParams& p, hipStream_t s) {
   const DmaDivs dv{fast_div(p.Wo), fast_div(p.Ho), fast_div(p.To), fast_div(nt)};
   const int n_split = p.n_split > 1 ? p.n_split : 1;
   const dim3 grid(mt * nt * n_split);
-  // the epilogue flags at compile time (split-K partials ignore them)
-  switch (n_split > 1 ? 0 : (p.res ? 1 : 0) | (p.relu ? 2 : 0) | (p.y_c8 ? 4 : 0)) {
+  // the epilogue flags at compile time (split-K partials ignore them); the buffer-offset DMAs where
+  // every tensor fits them
+  const int ef = n_split > 1 ? 0 : (p.res ? 1 : 0) | (p.relu ? 2 : 0) | (p.y_c8 ? 4 : 0);
+  switch (dma_x3_buf_ok(p, nt * BN) ? ef + 8 : ef) {
     case 0: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 0>), grid, dim3(256), 0, s, p, nt, dv); break;
     case 1: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 1>), grid, dim3(256), 0, s, p, nt, dv); break;
     case 2: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 2>), grid, dim3(256), 0, s, p, nt, dv); break;
     case 3: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 3>), grid, dim3(256), 0, s, p, nt, dv); break;
-    default: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN>), grid, dim3(256), 0, s, p, nt, dv); break;
+    case 8: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 0, 0, true>), grid, dim3(256), 0, s, p, nt, dv); break;
+    case 9: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 1, 0, true>), grid, dim3(256), 0, s, p, nt, dv); break;
+    case 10: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 2, 0, true>), grid, dim3(256), 0, s, p, nt, dv); break;
+    case 11: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 3, 0, true>), grid, dim3(256), 0, s, p, nt, dv); break;
+    default:
+      if (ef >= 8 || ef < 4) return hipErrorInvalidValue;
+      if (dma_x3_buf_ok(p, nt * BN))
+        hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, -1, 0, true>), grid, dim3(256), 0, s, p, nt, dv);
+      else
+        hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN>), grid, dim3(256), 0, s, p, nt, dv);
+      break;
   }
   if (n_split > 1) return launch_split_sum(p, s);
   return hipGetLastError();
@@ -1124,6 +1235,39 @@ hipError_t launch_dma_x3_cfg(const ConvParams& p, int mt, int nt, int S, hipStre
     case 182: return launch_dma_x3_t<1, 8, 2>(p, s);
   }
   return launch_dma_x3(p, 16 * nt, s);
+}
+
+template <int NT, int KO>
+static hipError_t dma_x3_ko_t(const ConvParams& p, hipStream_t s) {
+  const int mt = (p.M + 127) / 128, nt = (p.Cout + 16 * NT - 1) / (16 * NT);
+  const DmaDivs dv{fast_div(p.Wo), fast_div(p.Ho), fast_div(p.To), fast_div(nt)};
+  hipLaunchKernelGGL((conv_dma_x3<2, NT, 2, 1, 2, (KO & 31), (KO & 32) != 0>), dim3(mt * nt), dim3(256), 0, s, p, nt, dv);
+  return hipGetLastError();
+}
+// conv_dma_x3 knock-outs (KO bits of conv_dma_x3; + 32: the BUF form) at MT 2, 2 stages, the ReLU
+// epilogue, N tile 16 nt
+hipError_t launch_dma_x3_ko(const ConvParams& p, int nt, int ko, hipStream_t s) {
+  if (!dma_x3_supported(p) || p.res || !p.relu || p.y_c8 || p.n_split > 1) return hipErrorInvalidValue;
+#define DX3KO(N)                                       \
+  switch (ko) {                                        \
+    case 0: return dma_x3_ko_t<N, 0>(p, s);             \
+    case 1: return dma_x3_ko_t<N, 1>(p, s);             \
+    case 2: return dma_x3_ko_t<N, 2>(p, s);             \
+    case 4: return dma_x3_ko_t<N, 4>(p, s);             \
+    case 8: return dma_x3_ko_t<N, 8>(p, s);             \
+    case 16: return dma_x3_ko_t<N, 16>(p, s);           \
+    case 31: return dma_x3_ko_t<N, 31>(p, s);           \
+    case 32: return dma_x3_ko_t<N, 32>(p, s);           \
+    case 33: return dma_x3_ko_t<N, 33>(p, s);           \
+    case 34: return dma_x3_ko_t<N, 34>(p, s);           \
+    case 36: return dma_x3_ko_t<N, 36>(p, s);           \
+    case 40: return dma_x3_ko_t<N, 40>(p, s);           \
+    case 48: return dma_x3_ko_t<N, 48>(p, s);           \
+  }
+  if (nt == 5) DX3KO(5)
+  if (nt == 8) DX3KO(8)
+#undef DX3KO
+  return hipErrorInvalidValue;
 }
 #endif
 

@@ -125,6 +125,7 @@ int env_variants() {
   if (on("CLASFV_NO_PROJ_X3")) f |= CLASFV_VARIANT_NO_PROJ_X3;
   if (on("CLASFV_NO_WINO4R")) f |= CLASFV_VARIANT_NO_WINO4R;
   if (on("CLASFV_DECODER_ROWS16")) f |= CLASFV_VARIANT_DECODER_ROWS16;
+  if (on("CLASFV_NO_DMA_BUF")) f |= CLASFV_VARIANT_NO_DMA_BUF;
   return f;
 }
 
@@ -892,7 +893,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0x3FFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~0x7FFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;

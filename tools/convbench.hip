@@ -23,6 +23,7 @@ hipError_t launch_wino4_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_wino4w_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winor_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_dma_x3_cfg(const ConvParams& p, int mt, int nt, int S, hipStream_t s);
+hipError_t launch_dma_x3_ko(const ConvParams& p, int nt, int ko, hipStream_t s);
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
 hipError_t launch_patch_bf16_v1(const ConvParams& p, hipStream_t s);
 hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
@@ -121,6 +122,7 @@ int main(int argc, char** argv) {
   p.Kp = bf ? (p.K + 31) / 32 * 32 : (p.K + 15) / 16 * 16;
   p.M = N * p.To * p.Ho * p.Wo;
   p.relu = 1;
+  if (getenv("CLASFV_NO_DMA_BUF")) p.vflags |= CLASFV_VARIANT_NO_DMA_BUF;  // conv_dma_x3's pointer-form DMAs
   if (getenv("CB_STAGGER")) p.patch_nt = atoi(getenv("CB_STAGGER"));
   if (getenv("CB_C8") && winot) p.x_c8 = 1;  // 8-channel-blocked input (the engine's mid tensors)  // conv_wino4w ko 64: sleep units per phase
   const size_t nx = (size_t)N * T * H * W * Cin, ny = (size_t)p.M * Cout;
@@ -144,7 +146,7 @@ int main(int argc, char** argv) {
   // split-K into ko - 710 K ranges when >= 2
   void* wx3 = nullptr;
   for (int ko : kos)
-    if (!wino && !winot && !bf && ko >= 710 && ko < 720 && !wx3) {
+    if (!wino && !winot && !bf && ((ko >= 710 && ko < 720) || (ko >= 7200 && ko < 7264)) && !wx3) {
       std::vector<float> wf(nw);
       CK(hipMemcpy(wf.data(), p.w, nw * 4, hipMemcpyDeviceToHost));
       std::vector<uint16_t> img(dma_x3_weight_elems(Cout, p.Kp));
@@ -195,7 +197,13 @@ int main(int argc, char** argv) {
       if (getenv("CB_MT")) mt = atoi(getenv("CB_MT"));
       ConvParams q = p;
       if (ko >= 700 && ko < 709) q.n_split = ko - 700;  // conv_dma split-K into ko - 700 K ranges
-      if (ko >= 710 && ko < 720) {
+      if (ko >= 7200 && ko < 7264) {  // conv_dma_x3 knock-outs (KO = ko - 7200; + 32 the BUF form), N tile of CB_X3CFG's NT
+        q.w = wx3;
+        const char* cfg = getenv("CB_X3CFG");
+        int xm = 2, xn = dma_x3_bn(Cout) / 16, xs = 2;
+        if (cfg && *cfg) sscanf(cfg, "%d %d %d", &xm, &xn, &xs);
+        CK(launch_dma_x3_ko(q, xn, ko - 7200, s));
+      } else if (ko >= 710 && ko < 720) {
         q.w = wx3;
         q.n_split = ko - 710;
         const char* cfg = getenv("CB_X3CFG");  // "MT NT S"
