@@ -543,16 +543,38 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
     auto body = [&](auto rh_c, auto ch_c, auto r_c) __attribute__((always_inline)) {
       constexpr int RH = decltype(rh_c)::value, CH = decltype(ch_c)::value, RR = decltype(r_c)::value;
       f32x2 tt[6];
+      if constexpr (CPB == 0) {
+        // software-pipelined: column c + 1's window reads are issued before column c's row transform,
+        // so one LDS round trip is exposed per chunk instead of six (two columns' reads live at once)
+        auto col_read = [&](int c, f32x2 (&e)[5]) __attribute__((always_inline)) {
+          const int co = (c + (c >> 2)) * 16;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        const int co = (c + (c >> 2)) * 16;  // pixel columns 0..5 of the window -> slots 0,1,2,3,5,6
-        f32x2 e[5];
+          for (int q = 0; q < 5; ++q) e[q] = *reinterpret_cast<const f32x2*>(base + q * rp16 + co);
+        };
+        f32x2 e0[5], e1[5];
+        col_read(0, e0);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int q = 0; q < 5; ++q) e[q] = *reinterpret_cast<const f32x2*>(base + q * rp16 + co);
-        tt[c] = bt_row<RH, RR>(e);
-        // CPB columns' window reads in flight at a time: 168 registers hold 108 accumulators and the
-        // U ring (hoisting every column's reads spilled)
-        if (c % CPB == CPB - 1) __builtin_amdgcn_sched_barrier(0);
+        for (int c = 0; c < 6; c += 2) {
+          if (c + 1 < 6) col_read(c + 1, e1);
+          tt[c] = bt_row<RH, RR>(e0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (c + 2 < 6) col_read(c + 2, e0);
+          tt[c + 1] = bt_row<RH, RR>(e1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          const int co = (c + (c >> 2)) * 16;  // pixel columns 0..5 of the window -> slots 0,1,2,3,5,6
+          f32x2 e[5];
+#pragma unroll
+          for (int q = 0; q < 5; ++q) e[q] = *reinterpret_cast<const f32x2*>(base + q * rp16 + co);
+          tt[c] = bt_row<RH, RR>(e);
+          // CPB columns' window reads in flight at a time: 168 registers hold 108 accumulators and the
+          // U ring (hoisting every column's reads spilled)
+          if (c % CPB == CPB - 1) __builtin_amdgcn_sched_barrier(0);
+        }
       }
       bt_cols<CH>(tt, a);
     };
@@ -1026,6 +1048,7 @@ hipError_t launch_wino4r_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 64: return launch_w4r<9, 0, 6>(p, g, nb, s);     // 6-stage ring, a barrier every 3 chunks
     case 32: return launch_w4r<9, 0, 4, 2>(p, g, nb, s);  // 2 window columns' LDS reads in flight
     case 96: return launch_w4r<9, 0, 4, 3>(p, g, nb, s);  // 3
+    case 160: return launch_w4r<9, 0, 4, 0>(p, g, nb, s);  // software-pipelined column reads
     case 576: return launch_w4r<9, 512, 6>(p, g, nb, s);  // the same with stamps
     default: return launch_w4r<9>(p, g, nb, s);
   }

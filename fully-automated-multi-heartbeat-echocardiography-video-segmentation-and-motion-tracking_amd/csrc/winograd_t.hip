@@ -279,7 +279,7 @@ struct T5 {
 // bit 2 = split-K partial: the block sums input-channel chunks [k0, k1) of its split only and stores
 // y = A^T M without bias, residual or ReLU to p.part[split] (launch_split_sum finishes).
 template <int TS, int NT, int EPI>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_winot5(ConvParams p, int n_co,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((EPI & 16384) ? 3 : 2, (EPI & 16384) ? 3 : 2))) void conv_winot5(ConvParams p, int n_co,
                                                                                              int n_seg, int n_cols,
                                                                                              FastDiv fd_hw) {
   using G = T5<TS, NT>;
@@ -637,6 +637,7 @@ hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 817: return winot5_launch_e<4, 4, 3 + 4096>(p, s);   // (residual form)
     case 833: return winot5_launch_e<4, 4, 3 + 8192>(p, s);
     case 502: return winot5_dispatch(p, s, 2);
+    case 503: return p.res ? winot5_launch_e<4, 2, 3 + 16384>(p, s) : winot5_launch_e<4, 2, 2 + 16384>(p, s);  // NT 2, three waves per SIMD
     case 504: return winot5_dispatch(p, s, 4);
   }
   if (ko >= 600 && ko < 700 && p.part && !p.x_c8) {  // split-K: 6 NT S (p.part holds 8 partials)
