@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
 // fp32 as lo.hi + hi.lo + mid.mid + mid.hi + hi.mid + hi.hi (smallest first; the dropped terms are
 // below 2^-24 of the product), i.e. fp32-accurate, at 6 x 16 instead of 8 x 32 MFMA cycles per
 // 32-deep K block (2.67x the fp32 MFMA rate). The weights are split on the host into a bf16 image
-// [Cout_alloc][Kp/32][3 pieces][32] (dma_x3_weight_image); the activations are LDS-DMA'd as fp32
+// [Kp/32][3 pieces][Cout][32] (dma_x3_weight_image); the activations are LDS-DMA'd as fp32
 // exactly as in conv_dma and split in registers.
 //
 // A ring stage holds one K pair = two 16-channel steps: A as two fp32 tiles of conv_dma's layout
@@ -433,9 +433,9 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
     const int idx = wid + 4 * j;  // B instruction: piece idx / NT, rows 16 (idx % NT) ..
     const int pc = idx / NT, nr = idx - pc * NT;
     if constexpr (BUF)
-      b_bo[j] = idx < B_INS ? (unsigned)(((n0 + nr * 16 + drow) * npairs * 3 + pc) * 64 + 16 * dq) : 0u;
+      b_bo[j] = idx < B_INS ? (unsigned)((pc * p.Cout + n0 + nr * 16 + drow) * 64 + 16 * dq) : 0u;
     else
-      d_wrow[j] = idx < B_INS ? w + ((size_t)(n0 + nr * 16 + drow) * npairs * 3 + pc) * 32 + 8 * dq : w;
+      d_wrow[j] = idx < B_INS ? w + ((size_t)pc * p.Cout + n0 + nr * 16 + drow) * 32 + 8 * dq : w;
   }
   // BUF: per A row, the tap-validity bits (tap = (kt KH + kh) KW + kw; 0 for a row past M) and the
   // byte offsets of its first tap's pixel in x and x2 (16-B slot dq included)
@@ -448,7 +448,7 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
   const __amdgpu_buffer_rsrc_t x2r = __builtin_amdgcn_make_buffer_rsrc(
       BUF && x2 ? const_cast<float*>(x2) : nullptr, (short)0, BUF && x2 ? (int)(vox * p.Cin2 * 4) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      BUF ? const_cast<__bf16*>(w) : nullptr, (short)0, BUF ? (int)((size_t)n_tiles * BN * npairs * 192) : 0, 0x00020000);
+      BUF ? const_cast<__bf16*>(w) : nullptr, (short)0, BUF ? (int)((size_t)p.Cout * npairs * 192) : 0, 0x00020000);
   if constexpr (BUF) {
 #pragma unroll
     for (int j = 0; j < A_PER; ++j) {
@@ -543,10 +543,10 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
       if constexpr (BUF) {
         // (offsets through locals: a captured array element as the builtin's operand made the host-side
         // instantiation fail substitution)
-        const unsigned bo = b_bo[j], so = (unsigned)pair * 192u;
+        const unsigned bo = b_bo[j], so = (unsigned)pair * (unsigned)(192 * p.Cout);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)dst, 16, bo, so, 0, 0);
       } else {
-        const void* src = idx < B_INS ? (const void*)(d_wrow[j] + (size_t)pair * 96) : p.zero;
+        const void* src = idx < B_INS ? (const void*)(d_wrow[j] + (size_t)pair * 96 * p.Cout) : p.zero;
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                          (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
       }
@@ -664,7 +664,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int drow = lane >> 2, dq = (lane & 3) ^ G[(drow >> 2) & 3];
     for (int j = wid; j < PIECES; j += 4) {
       const int nt = j & 3, pc = (j >> 2) % 3, kb = j / 12;
-      const __bf16* src = w + ((size_t)(16 * nt + drow) * KB * 3 + (size_t)kb * 3 + pc) * 32 + 8 * dq;
+      const __bf16* src = w + (((size_t)kb * 3 + pc) * p.Cout + 16 * nt + drow) * 32 + 8 * dq;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(smem + j * 1024), 16, 0, 0);
     }
@@ -1271,10 +1271,12 @@ hipError_t launch_dma_x3_ko(const ConvParams& p, int nt, int ko, hipStream_t s) 
 }
 #endif
 
-// bf16 image [cout_alloc][npairs][3][32] of an fp32 [cout_alloc][Kp] weight image (Kp % 16 == 0,
+// bf16 image [npairs][3][cout_alloc][32] of an fp32 [cout_alloc][Kp] weight image (Kp % 16 == 0,
 // npairs = ceil(Kp / 32)): piece pc of element (n, k) is the bf16 of w - (pieces < pc) (round to
 // nearest, exact in double); element 8q + e of a 32-slot holds k = 32 pair + 4q + e (e < 4) or
-// 32 pair + 16 + 4q + (e - 4) -- conv_dma_x3's operand order.
+// 32 pair + 16 + 4q + (e - 4) -- conv_dma_x3's operand order. Pair- and piece-major (round 5; was
+// [cout_alloc][npairs][3][32]): the 16 rows one B-piece DMA instruction fetches are 1 KiB contiguous
+// instead of 16 half-lines npairs * 192 B apart.
 void dma_x3_weight_image(const float* w, int cout_alloc, int Kp, uint16_t* out) {
   const int npairs = (Kp / 16 + 1) / 2;
   for (int n = 0; n < cout_alloc; ++n)
@@ -1292,7 +1294,7 @@ void dma_x3_weight_image(const float* w, int cout_alloc, int Kp, uint16_t* out) 
           const uint32_t ub = (uint32_t)b << 16;
           float fb;
           memcpy(&fb, &ub, 4);
-          out[(((size_t)n * npairs + pr) * 3 + pc) * 32 + sl] = b;
+          out[(((size_t)pr * 3 + pc) * cout_alloc + n) * 32 + sl] = b;
           r -= fb;
         }
       }

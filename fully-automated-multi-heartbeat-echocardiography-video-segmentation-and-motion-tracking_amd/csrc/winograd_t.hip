@@ -520,38 +520,51 @@ hipError_t winot5_launch_e(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int TS, int NT>
+// W3 (NT = 2 only): three waves per SIMD (EPI bit 16384: 160 VGPRs, three 48 KiB blocks per CU)
+template <int TS, int NT, bool W3 = false>
 hipError_t winot5_launch(const ConvParams& p, hipStream_t s) {
+  constexpr int X = W3 ? 16384 : 0;
   if (p.n_split > 1) {
-    hipError_t e = winot5_launch_e<TS, NT, 4>(p, s);  // bias, residual and ReLU in the sum pass
+    hipError_t e = winot5_launch_e<TS, NT, 4 + X>(p, s);  // bias, residual and ReLU in the sum pass
     if (e != hipSuccess) return e;
     return launch_split_sum(p, s);
   }
   switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
-    case 2: return winot5_launch_e<TS, NT, 2>(p, s);  // TP1 / stem T: BN + ReLU
-    case 3: return winot5_launch_e<TS, NT, 3>(p, s);  // TP2: BN + residual + ReLU
-    case 1: return winot5_launch_e<TS, NT, 1>(p, s);
-    default: return winot5_launch_e<TS, NT, 0>(p, s);
+    case 2: return winot5_launch_e<TS, NT, 2 + X>(p, s);  // TP1 / stem T: BN + ReLU
+    case 3: return winot5_launch_e<TS, NT, 3 + X>(p, s);  // TP2: BN + residual + ReLU
+    case 1: return winot5_launch_e<TS, NT, 1 + X>(p, s);
+    default: return winot5_launch_e<TS, NT, 0 + X>(p, s);
   }
 }
 
-// 64 channels per wave (NT = 4); 32 when that leaves fewer than two blocks per CU (layer3 maps).
+// Channels per wave: 64 (NT = 4, two blocks per CU: 512 slots) or 32 (NT = 2 at three waves per SIMD,
+// three blocks per CU: 768 slots), whichever fills its last wave of blocks better, NT = 2 priced at
+// its measured 5.4 % more time per output on a full chip (profiles/r05v_winot_nt2_three_waves.txt:
+// 0.832 vs 0.789 ms). Layer3 at 30 clips: 736 NT-4 blocks fill 1.44 waves (0.72), 1472 NT-2 blocks
+// 1.92 (0.96 / 1.054 = 0.91). Both forms compute the same products in the same order
+// (bit-identical), so the batch-dependent choice does not change a clip's result. Returns 4, 2 or 3
+// (NT = 2 at three waves per SIMD); *blocks: the launch's blocks.
 int winot5_nt(const ConvParams& p, long* blocks) {
   const int tt = p.Ti / 4;
   const int ts = tt % 4 == 0 ? 4 : tt % 2 == 0 ? 2 : 1;
-  const long blocks64 = (long)((p.N * p.Hi * p.Wi + 16 * 8 / ts - 1) / (16 * 8 / ts)) * (tt / ts) * (p.Cout / 64);
-  const int nt = blocks64 >= 512 ? 4 : 2;
-  if (blocks) *blocks = blocks64 * (4 / nt);
-  return nt;
+  const long b4 = (long)((p.N * p.Hi * p.Wi + 16 * 8 / ts - 1) / (16 * 8 / ts)) * (tt / ts) * (p.Cout / 64);
+  const long b2 = 2 * b4;
+  const double fill4 = (double)b4 / (double)(((b4 + 511) / 512) * 512);
+  const double fill2 = (double)b2 / (double)(((b2 + 767) / 768) * 768) / 1.054;
+  // (TS = 1: three 60 KiB NT-2 blocks do not fit a CU's LDS; the two-wave NT-2 form below 512 blocks)
+  const int nt = ts == 1 ? (b4 >= 512 ? 4 : 2) : fill2 > fill4 ? 3 : 4;
+  if (blocks) *blocks = nt == 4 ? b4 : b2;
+  return nt;  // (ts == 1 never returns 3)
 }
 
+// force_nt (tools/convbench): 4, 2 (NT = 2 at two waves per SIMD) or 3 (NT = 2 at three)
 hipError_t winot5_dispatch(const ConvParams& p, hipStream_t s, int force_nt = 0) {
   const int tt = p.Ti / 4;
   const int ts = tt % 4 == 0 ? 4 : tt % 2 == 0 ? 2 : 1;
   const int nt = force_nt ? force_nt : winot5_nt(p, nullptr);
-  if (ts == 4) return nt == 4 ? winot5_launch<4, 4>(p, s) : winot5_launch<4, 2>(p, s);
-  if (ts == 1) return nt == 4 ? winot5_launch<1, 4>(p, s) : winot5_launch<1, 2>(p, s);
-  return nt == 4 ? winot5_launch<2, 4>(p, s) : winot5_launch<2, 2>(p, s);
+  if (ts == 4) return nt == 4 ? winot5_launch<4, 4>(p, s) : nt == 3 ? winot5_launch<4, 2, true>(p, s) : winot5_launch<4, 2>(p, s);
+  if (ts == 1) return nt == 4 ? winot5_launch<1, 4>(p, s) : nt == 3 ? winot5_launch<1, 2, true>(p, s) : winot5_launch<1, 2>(p, s);
+  return nt == 4 ? winot5_launch<2, 4>(p, s) : nt == 3 ? winot5_launch<2, 2, true>(p, s) : winot5_launch<2, 2>(p, s);
 }
 
 // conv_winot5 addresses its input with 32-bit byte offsets from the chunk's scalar base
@@ -637,7 +650,7 @@ hipError_t launch_winot_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 817: return winot5_launch_e<4, 4, 3 + 4096>(p, s);   // (residual form)
     case 833: return winot5_launch_e<4, 4, 3 + 8192>(p, s);
     case 502: return winot5_dispatch(p, s, 2);
-    case 503: return p.res ? winot5_launch_e<4, 2, 3 + 16384>(p, s) : winot5_launch_e<4, 2, 2 + 16384>(p, s);  // NT 2, three waves per SIMD
+    case 503: return winot5_dispatch(p, s, 3);  // NT 2, three waves per SIMD
     case 504: return winot5_dispatch(p, s, 4);
   }
   if (ko >= 600 && ko < 700 && p.part && !p.x_c8) {  // split-K: 6 NT S (p.part holds 8 partials)
