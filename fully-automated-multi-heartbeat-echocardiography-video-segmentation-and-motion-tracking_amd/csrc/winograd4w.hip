@@ -469,7 +469,7 @@ __device__ inline f32x2 bt_row(const f32x2 (&e)[5]) {
 // KO (tools/convbench diagnostics, 0 in the product; results wrong otherwise): 1 no transform, 2 no U
 // loads in the loop, 4 no epilogue, 8 no loop DMAs, 16 no chunk barriers, 128 no output stores, 512
 // per-block phase stamps (as conv_wino4w's). NR: raw ring stages (4: a barrier every 2 chunks; 6: every 3)
-template <int NTN, bool C8, int KO = 0, bool RELU = true, int NR = W4R_NR, int CPB = 1>
+template <int NTN, bool C8, int KO = 0, bool RELU = true, int NR = W4R_NR, int CPB = 1, bool NTS = false>
 __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3))) void conv_wino4r(ConvParams p,
                                                                                                        W4Geo g) {
   using WR = W4R<NTN>;
@@ -762,6 +762,8 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
       float* dst = ybase[aa] + nt * nt_step;
       if constexpr ((KO & 128) != 0) {
         if (o[0] == 1234.5f) *reinterpret_cast<f32x4*>(dst) = o;
+      } else if constexpr (NTS || (KO & 2048) != 0) {  // non-temporal output stores (the product form)
+        __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(dst));
       } else {
         *reinterpret_cast<f32x4*>(dst) = o;
       }
@@ -804,6 +806,20 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
 template <int NTN, int KO = 0, int NR = W4R_NR, int CPB = 1>
 hipError_t launch_w4r(const ConvParams& p, const W4Geo& g, int n_blocks, hipStream_t s) {
   const dim3 grid(n_blocks), block(W4R_THREADS);
+  // non-temporal output stores unless CLASFV_VARIANT_W4R_CACHED_STORES (the ReLU / C8 forms the forward
+  // runs): the 144-channel mid tensor is streamed past L2 / MALL, and both this kernel and the temporal
+  // Winograd that reads it next run faster (profiles/r05ab_w4r_nt_stores_ab.txt: wino4r 9.11 -> 9.05,
+  // winot 5.46 -> 5.38 ms per forward, step 21.57 -> 21.38 ms)
+  if (!(p.vflags & CLASFV_VARIANT_W4R_CACHED_STORES)) {
+    if (p.y_c8 && p.relu) {
+      hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, true, NR, CPB, true>), grid, block, 0, s, p, g);
+      return hipGetLastError();
+    }
+    if (p.relu) {
+      hipLaunchKernelGGL((conv_wino4r<NTN, false, KO, true, NR, CPB, true>), grid, block, 0, s, p, g);
+      return hipGetLastError();
+    }
+  }
   if (p.y_c8 && p.relu)
     hipLaunchKernelGGL((conv_wino4r<NTN, true, KO, true, NR, CPB>), grid, block, 0, s, p, g);
   else if (p.relu)
@@ -1049,6 +1065,7 @@ hipError_t launch_wino4r_ko(const ConvParams& p, hipStream_t s, int ko) {
     case 32: return launch_w4r<9, 0, 4, 2>(p, g, nb, s);  // 2 window columns' LDS reads in flight
     case 96: return launch_w4r<9, 0, 4, 3>(p, g, nb, s);  // 3
     case 160: return launch_w4r<9, 0, 4, 0>(p, g, nb, s);  // software-pipelined column reads
+    case 2048: return launch_w4r<9, 2048>(p, g, nb, s);    // non-temporal output stores
     case 576: return launch_w4r<9, 512, 6>(p, g, nb, s);  // the same with stamps
     default: return launch_w4r<9>(p, g, nb, s);
   }

@@ -494,7 +494,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((EPI & 1638
 #pragma unroll
             for (int c = 0; c < 4; ++c) vv[c] = relu1(vv[c]);
           }
-          *reinterpret_cast<f32x4*>(yout + o + a2 * fstride) = vv;
+          if constexpr ((EPI & 32768) != 0)
+            __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(yout + o + a2 * fstride));
+          else
+            *reinterpret_cast<f32x4*>(yout + o + a2 * fstride) = vv;
         }
       }
     }
@@ -528,6 +531,10 @@ hipError_t winot5_launch(const ConvParams& p, hipStream_t s) {
     hipError_t e = winot5_launch_e<TS, NT, 4 + X>(p, s);  // bias, residual and ReLU in the sum pass
     if (e != hipSuccess) return e;
     return launch_split_sum(p, s);
+  }
+  if (p.vflags & CLASFV_VARIANT_WINOT_NT_STORES) {  // A/B: non-temporal output stores
+    if (p.res && p.relu) return winot5_launch_e<TS, NT, 3 + X + 32768>(p, s);
+    if (p.relu) return winot5_launch_e<TS, NT, 2 + X + 32768>(p, s);
   }
   switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
     case 2: return winot5_launch_e<TS, NT, 2 + X>(p, s);  // TP1 / stem T: BN + ReLU

@@ -79,7 +79,9 @@ enum {
   CLASFV_VARIANT_NO_PROJ_X3 = 32768,   /* CLASFV_NO_PROJ_X3: the decoder's 128-deep tap projections on conv_dma_x3 instead of the persistent conv_proj_x3 */
   CLASFV_VARIANT_NO_WINO4R = 65536,    /* CLASFV_NO_WINO4R: wide-block 1x3x3 convs on conv_wino4w (4 quadrant waves, one per SIMD) instead of conv_wino4r (12 row waves, three per SIMD) */
   CLASFV_VARIANT_DECODER_ROWS16 = 131072, /* CLASFV_DECODER_ROWS16: the fp32 engines' decoder on 16 x 16-voxel tiles instead of 8 x 16 (bit-identical; 1 % slower in the forward) */
-  CLASFV_VARIANT_NO_DMA_BUF = 262144   /* CLASFV_NO_DMA_BUF: conv_dma_x3's LDS-DMAs from 64-bit pointers instead of 32-bit buffer offsets */
+  CLASFV_VARIANT_NO_DMA_BUF = 262144,  /* CLASFV_NO_DMA_BUF: conv_dma_x3's LDS-DMAs from 64-bit pointers instead of 32-bit buffer offsets */
+  CLASFV_VARIANT_W4R_CACHED_STORES = 524288, /* CLASFV_W4R_CACHED_STORES: conv_wino4r's output stores cached instead of non-temporal */
+  CLASFV_VARIANT_WINOT_NT_STORES = 1048576  /* CLASFV_WINOT_NT_STORES: conv_winot5's output stores non-temporal (A/B) */
 };
 
 typedef struct clasfv_engine* clasfv_t;
