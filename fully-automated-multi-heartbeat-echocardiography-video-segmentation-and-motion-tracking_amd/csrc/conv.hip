@@ -69,7 +69,12 @@ __device__ inline f32x4 load_res4(const void* res, size_t o, int bf16) {
   return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(res) + o);
 }
 
+template <bool NTS = false>
 __device__ inline void store_out4(void* y, size_t o, f32x4 v, int bf16) {
+  if constexpr (NTS) {  // non-temporal (fp32 outputs only)
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(reinterpret_cast<float*>(y) + o));
+    return;
+  }
   if (bf16)
     *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(y) + o) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
   else
@@ -86,7 +91,7 @@ __device__ inline void store_out4(void* y, size_t o, f32x4 v, int bf16) {
 // vector-memory op (vmcnt retires in order), and the compiler's own waits in the per-element
 // branches were vmcnt(0): the per-element form paid the store latency once per (row, N tile) --
 // MT x NT times per block. Bigger residual tiles load one row at a time (one wait per row).
-template <int MT, int NT, int EF = -1>
+template <int MT, int NT, int EF = -1, bool NTS = false>
 __device__ inline void epilogue(const ConvParams& p, const f32x4 (&acc)[MT][NT], int m_base, int n0, int q, int l16) {
   const bool has_res = EF < 0 ? p.res != nullptr : (EF & 1) != 0;
   const bool relu = EF < 0 ? p.relu != 0 : (EF & 2) != 0;
@@ -140,7 +145,7 @@ __device__ inline void epilogue(const ConvParams& p, const f32x4 (&acc)[MT][NT],
 #pragma unroll
         for (int c = 0; c < 4; ++c) v[c] = relu1(v[c]);
       }
-      store_out4(p.y, off(m, n), v, obf);
+      store_out4<NTS>(p.y, off(m, n), v, obf);
     }
   }
 }
@@ -378,7 +383,7 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
 // KO (tools/convbench timing knock-outs, 0 in the product; results wrong otherwise): 1 no activation
 // split (the fp32 bits reinterpreted as the three pieces), 2 no B-piece LDS reads, 4 no DMAs in the
 // loop, 8 no waits / barriers, 16 no epilogue.
-template <int MT, int NT, int S, int WN = 1, int EF = -1, int KO = 0, bool BUF = false>
+template <int MT, int NT, int S, int WN = 1, int EF = -1, int KO = 0, bool BUF = false, bool NTS = false>
 __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, DmaDivs dv) {
   static_assert(NT % WN == 0, "N tiles split evenly over the waves along N");
   constexpr int MTW = MT * WN, NTW = NT / WN;  // 16 x 16 tiles per wave
@@ -631,7 +636,7 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
     partial_store<MTW, NTW>(p, acc, p.part + (size_t)split * p.M * p.Cout, m0 + wm * 16 * MTW, n0 + wn * 16 * NTW, q,
                             l16);
   else
-    epilogue<MTW, NTW, EF>(p, acc, m0 + wm * 16 * MTW, n0 + wn * 16 * NTW, q, l16);
+    epilogue<MTW, NTW, EF, NTS>(p, acc, m0 + wm * 16 * MTW, n0 + wn * 16 * NTW, q, l16);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1007,6 +1012,13 @@ hipError_t launch_dma_x3_t(const ConvParams& p, hipStream_t s) {
   // the epilogue flags at compile time (split-K partials ignore them); the buffer-offset DMAs where
   // every tensor fits them
   const int ef = n_split > 1 ? 0 : (p.res ? 1 : 0) | (p.relu ? 2 : 0) | (p.y_c8 ? 4 : 0);
+  if ((p.vflags & CLASFV_VARIANT_DMA_NT_STORES) && n_split == 1 && dma_x3_buf_ok(p, nt * BN) && (ef == 2 || ef == 3)) {
+    if (ef == 2)
+      hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 2, 0, true, true>), grid, dim3(256), 0, s, p, nt, dv);
+    else
+      hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 3, 0, true, true>), grid, dim3(256), 0, s, p, nt, dv);
+    return hipGetLastError();
+  }
   switch (dma_x3_buf_ok(p, nt * BN) ? ef + 8 : ef) {
     case 0: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 0>), grid, dim3(256), 0, s, p, nt, dv); break;
     case 1: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 1>), grid, dim3(256), 0, s, p, nt, dv); break;

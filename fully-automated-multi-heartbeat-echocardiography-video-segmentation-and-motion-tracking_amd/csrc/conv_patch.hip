@@ -324,7 +324,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
           if constexpr (G::SPATIAL) ok = to < p.To && h0 + px0 / 8 + (v >> 3) < p.Ho && w0 + (v & 7) < p.Wo;
           else ok = to < p.To && hw0 + px0 + v < HW;
         }
-        if (ok) *reinterpret_cast<bf16x8*>(yb + lo) = val;
+        if (ok) {
+          if constexpr (EF & 4) {
+            __builtin_nontemporal_store(val, reinterpret_cast<bf16x8*>(yb + lo));
+          } else {
+            *reinterpret_cast<bf16x8*>(yb + lo) = val;
+          }
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
       __builtin_amdgcn_wave_barrier();
@@ -369,6 +375,15 @@ hipError_t launch_pe(const ConvParams& p, hipStream_t s) {
 
 template <int NT, int KT, int FR, int S = 3, bool STG = true>
 hipError_t launch_p(const ConvParams& p, hipStream_t s) {
+  if constexpr (STG) {
+    // EF 4: non-temporal output stores (A/B variant CLASFV_PATCH_NT_STORES)
+    if (p.vflags & CLASFV_VARIANT_PATCH_NT_STORES) switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
+      case 0: return launch_pe<NT, KT, FR, S, STG, 4>(p, s);
+      case 1: return launch_pe<NT, KT, FR, S, STG, 5>(p, s);
+      case 2: return launch_pe<NT, KT, FR, S, STG, 6>(p, s);
+      default: return launch_pe<NT, KT, FR, S, STG, 7>(p, s);
+    }
+  }
   switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
     case 0: return launch_pe<NT, KT, FR, S, STG, 0>(p, s);
     case 1: return launch_pe<NT, KT, FR, S, STG, 1>(p, s);
@@ -767,7 +782,12 @@ bool patch32_bf16_supported(const ConvParams& p) {
 
 hipError_t launch_patch32_bf16(const ConvParams& p, hipStream_t s) {
   if (!patch32_bf16_supported(p)) return hipErrorInvalidValue;
-  switch (patch32_pick_nb(p, p.patch_nt < 0 ? -p.patch_nt : 0)) {  // CLASFV_PATCH_NT < 0: force NB
+  const int nb = patch32_pick_nb(p, p.patch_nt < 0 ? -p.patch_nt : 0);  // CLASFV_PATCH_NT < 0: force NB
+  // output stores non-temporal (MODE 64): the forward's bf16 A/B (profiles/r05ad_nt_stores_ab3.txt)
+  // 3151 / 3166 -> 3201 / 3203 clips/s, this kernel 2.03 -> 1.98 ms and its consumer conv_patch_bf16
+  // faster too; CLASFV_PATCH32_CACHED_STORES keeps the cached form
+  if (!(p.vflags & CLASFV_VARIANT_PATCH32_CACHED_STORES) && nb == 5) return launch_p32<5, 2, 1 | 64>(p, s);
+  switch (nb) {
     case 5: return launch_p32<5>(p, s);
     case 4: return launch_p32<4>(p, s);
     case 3: return launch_p32<3>(p, s);

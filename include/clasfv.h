@@ -81,7 +81,10 @@ enum {
   CLASFV_VARIANT_DECODER_ROWS16 = 131072, /* CLASFV_DECODER_ROWS16: the fp32 engines' decoder on 16 x 16-voxel tiles instead of 8 x 16 (bit-identical; 1 % slower in the forward) */
   CLASFV_VARIANT_NO_DMA_BUF = 262144,  /* CLASFV_NO_DMA_BUF: conv_dma_x3's LDS-DMAs from 64-bit pointers instead of 32-bit buffer offsets */
   CLASFV_VARIANT_W4R_CACHED_STORES = 524288, /* CLASFV_W4R_CACHED_STORES: conv_wino4r's output stores cached instead of non-temporal */
-  CLASFV_VARIANT_WINOT_NT_STORES = 1048576  /* CLASFV_WINOT_NT_STORES: conv_winot5's output stores non-temporal (A/B) */
+  CLASFV_VARIANT_WINOT_NT_STORES = 1048576, /* CLASFV_WINOT_NT_STORES: conv_winot5's output stores non-temporal (A/B) */
+  CLASFV_VARIANT_DMA_NT_STORES = 2097152,   /* CLASFV_DMA_NT_STORES: conv_dma_x3's output stores non-temporal (A/B) */
+  CLASFV_VARIANT_PATCH32_CACHED_STORES = 4194304, /* CLASFV_PATCH32_CACHED_STORES: conv_patch32_bf16's output stores cached (the product's are non-temporal) */
+  CLASFV_VARIANT_PATCH_NT_STORES = 8388608  /* CLASFV_PATCH_NT_STORES: conv_patch_bf16's output stores non-temporal (A/B) */
 };
 
 typedef struct clasfv_engine* clasfv_t;
