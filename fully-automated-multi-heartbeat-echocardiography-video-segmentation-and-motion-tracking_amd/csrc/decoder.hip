@@ -88,6 +88,20 @@ __device__ inline int xcd_swizzle_d(int b, int nb) {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// single-lane f32 FMA / multiply kept as one v_fma_f32 / v_mul_f32: on f32x4 values the compiler emits
+// v_pk_fma_f32 / v_pk_mul_f32, which beside other waves' MFMAs cost more issue than two scalar ops
+// (MI355X_MICROARCH.md, "packed f32 VALU: an anti-lever beside MFMAs")
+__device__ inline float fma1(float a, float b, float c) {
+  float d;
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ inline float mul1(float a, float b) {
+  float d;
+  asm("v_mul_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+
 __device__ inline bf16x8 to_bf16x8(f32x4 a, f32x4 b) {
   return bf16x8{(__bf16)a[0], (__bf16)a[1], (__bf16)a[2], (__bf16)a[3],
                 (__bf16)b[0], (__bf16)b[1], (__bf16)b[2], (__bf16)b[3]};
@@ -255,8 +269,12 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
 // split-bf16 products (the fp32 engines' default); timing knock-outs for tools/convbench.hip
 // (CLASFV_KNOCKOUTS builds only; wrong results): 2 = no comb_2 / head MFMAs, 3 = no interpolation.
 // TROWS: tile rows (8: 4 waves per block; 16: 8 waves, half the blocks and less halo per voxel)
-template <int MODE, int TROWS = 8>
-__global__ __launch_bounds__(32 * TROWS) __attribute__((amdgpu_waves_per_eu(MODE == 4 ? 4 : 5, MODE == 4 ? 4 : 5))) void decoder_kernel(DecParams p) {
+// MODE + 8 (SC): the staging blend and the interpolation as single-lane v_fma_f32 / v_mul_f32
+// (the same operations and order as the packed form, so bit-identical)
+template <int MODE_, int TROWS = 8>
+__global__ __launch_bounds__(32 * TROWS) __attribute__((amdgpu_waves_per_eu((MODE_ & 7) == 4 ? 4 : 5, (MODE_ & 7) == 4 ? 4 : 5))) void decoder_kernel(DecParams p) {
+  constexpr int MODE = MODE_ & 7;
+  constexpr bool SC = (MODE_ & 8) != 0;
   using G = DecGeo<TROWS>;
   constexpr int TILE_H = TROWS, NTHR = G::NTHR;
   constexpr int BF = MODE == 1 || MODE == 4;
@@ -340,7 +358,15 @@ __global__ __launch_bounds__(32 * TROWS) __attribute__((amdgpu_waves_per_eu(MODE
       const int e = tid + NTHR * k;
       if (live[G::kLiveOff[i] + k]) {
         f32x4 v = buf[G::kLoadOff[i] + k * G::kFrames[i]];
-        if (G::kFrames[i] == 2) v = v * w.lt0 + buf[G::kLoadOff[i] + k * G::kFrames[i] + 1] * w.lt1;
+        if (G::kFrames[i] == 2) {
+          const f32x4 v1 = buf[G::kLoadOff[i] + k * G::kFrames[i] + 1];
+          if constexpr (SC) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fma1(v[e], w.lt0, mul1(v1[e], w.lt1));
+          } else {
+            v = v * w.lt0 + v1 * w.lt1;
+          }
+        }
         *reinterpret_cast<f32x4*>(dst + (e >> 4) * PIX + (e & 15) * 4) = v;
       }
     }
@@ -395,17 +421,38 @@ __global__ __launch_bounds__(32 * TROWS) __attribute__((amdgpu_waves_per_eu(MODE
       const float wb = (yb0 - ya0 == k ? lb0 : 0.f) + (yb1 - ya0 == k ? lb1 : 0.f);
       const int ro = k * G::kMaxCols[i] * PIX;
       f32x4 hx[4];
+      if constexpr (SC) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        hx[c] = *reinterpret_cast<const f32x4*>(c0p + ro + 16 * c) * lx0 +
-                *reinterpret_cast<const f32x4*>(c1p + ro + 16 * c) * lx1;
-      if (ta) {
+        for (int c = 0; c < 4; ++c) {
+          const f32x4 a0 = *reinterpret_cast<const f32x4*>(c0p + ro + 16 * c), a1 = *reinterpret_cast<const f32x4*>(c1p + ro + 16 * c);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) h1[0][c] += hx[c] * wa;
-      }
-      if (tb) {
+          for (int e = 0; e < 4; ++e) hx[c][e] = fma1(a0[e], lx0, mul1(a1[e], lx1));
+        }
+        if (ta) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) h1[1][c] += hx[c] * wb;
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) h1[0][c][e] = fma1(hx[c][e], wa, h1[0][c][e]);
+        }
+        if (tb) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) h1[1][c][e] = fma1(hx[c][e], wb, h1[1][c][e]);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          hx[c] = *reinterpret_cast<const f32x4*>(c0p + ro + 16 * c) * lx0 +
+                  *reinterpret_cast<const f32x4*>(c1p + ro + 16 * c) * lx1;
+        if (ta) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) h1[0][c] += hx[c] * wa;
+        }
+        if (tb) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) h1[1][c] += hx[c] * wb;
+        }
       }
       // one source row's 8 LDS reads in flight at a time (hoisting more spills)
       __builtin_amdgcn_sched_barrier(0);
@@ -524,6 +571,8 @@ static hipError_t launch_dec(const DecParams& p, hipStream_t s, int mode, int th
 #ifdef CLASFV_KNOCKOUTS
   if (mode == 2) k = th == 16 ? decoder_kernel<2, 16> : decoder_kernel<2>;
   if (mode == 3) k = th == 16 ? decoder_kernel<3, 16> : decoder_kernel<3>;
+  if (mode == 12) k = th == 16 ? decoder_kernel<12, 16> : decoder_kernel<12>;
+  if (mode == 9) k = th == 16 ? decoder_kernel<9, 16> : decoder_kernel<9>;
 #endif
   hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(32 * th), lds, s, p);
   return hipGetLastError();
@@ -578,6 +627,7 @@ hipError_t launch_decoder(const DecParams& p, hipStream_t s) {
 // tools/convbench.hip: ko 0 = 8-row tiles; 2, 3 = decoder_kernel's knock-out modes; + 16: 16-row tiles
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko) {
   const int m = ko & 15;
-  return launch_dec(p, s, m == 2 || m == 3 ? m : (p.bf16 ? 1 : p.x3 ? 4 : 0), (ko & 16) ? 16 : 8);
+  const int base = m == 2 || m == 3 ? m : (p.bf16 ? 1 : p.x3 ? 4 : 0);
+  return launch_dec(p, s, (ko & 32) && (base == 1 || base == 4) ? base + 8 : base, (ko & 16) ? 16 : 8);
 }
 #endif
