@@ -18,6 +18,8 @@
 // MFMA form D^T = U^T V^T (weights as the A operand): an accumulator lane holds 4 consecutive output
 // channels of one tile, so the epilogue moves 16-B vectors through LDS in both directions (same
 // products and accumulation order as the V U form: bit-identical to conv_wino4).
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "wino4_common.h"
@@ -483,6 +485,17 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
   unsigned long long st_[4] = {0, 0, 0, 0};
   if constexpr ((KO & 512) != 0) st_[0] = __builtin_amdgcn_s_memrealtime();
 #endif
+  // start stagger (W4Geo::stagger): blocks of equal work started together stay in lockstep, and all
+  // 256 CUs then run their epilogues -- the output stores -- at once, reading nothing meanwhile
+  // (profiles/r05ag_wino4r_epilogue_concurrency.txt); first-round blocks 8 j .. 8 j + 7 (one per XCD)
+  // start (j % groups) stagger ticks apart, so the epilogues of different CUs fall in different phases
+  if (g.stagger > 0 && blockIdx.x < 256) {
+    const int sg = (blockIdx.x >> 3) % g.stagger_groups;
+    if (sg) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), dt = (unsigned long long)sg * g.stagger;
+      while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
+    }
+  }
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(p.x), (short)0, (int)((size_t)p.N * p.Ti * p.Hi * p.Wi * p.Cin * 4), 0x00020000);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1052,6 +1065,7 @@ hipError_t launch_wino4r_ko(const ConvParams& p, hipStream_t s, int ko) {
   W4Geo g;
   int nb;
   wino4_geometry(p, &g, &nb, 144, W4W_FILL);
+  if (const char* e = getenv("CB_W4R_STAGGER")) sscanf(e, "%d,%d", &g.stagger, &g.stagger_groups);  // ticks,groups
   switch (ko) {
     case 1: return launch_w4r<9, 1>(p, g, nb, s);
     case 2: return launch_w4r<9, 2>(p, g, nb, s);

@@ -284,6 +284,23 @@ int main(int argc, char** argv) {
         const char* names[6] = {"prologue", "chunk loop", "epilogue", "item-2 prologue", "item-2 chunk loop", "item-2 epilogue"};
         for (int i = 0; i < last; ++i) printf(" %s %.2f,", names[i], ph[i] / nb / 100.0);
         printf(" total %.2f; CU gap between blocks %.2f us\n", tot / nb / 100.0, ng ? gap / ng / 100.0 : 0.0);
+        // phase alignment across CUs: blocks in their epilogue (stamp 2 .. 3) at each 0.5-us sample of the
+        // middle 80 % of the run -- lockstep blocks give a bursty count (all CUs writing at once),
+        // de-phased ones a flat count near ncu x epilogue / block time
+        if (!two && nb > 0) {
+          const unsigned long long a0 = t_min + (t_max - t_min) / 10, a1 = t_max - (t_max - t_min) / 10;
+          std::vector<int> cnt((size_t)((a1 - a0) / 50 + 1), 0);
+          for (int b = 0; b < nb; ++b)
+            for (unsigned long long t = S(b, 2); t < S(b, 3); t += 1)
+              if (t >= a0 && t < a1 && (t - a0) % 50 == 0) ++cnt[(t - a0) / 50];
+          std::vector<int> sc = cnt;
+          std::sort(sc.begin(), sc.end());
+          double mean = 0;
+          for (int c : sc) mean += c;
+          mean /= sc.size();
+          printf("epilogue concurrency (blocks per 0.5-us sample): mean %.1f, p10 %d, p50 %d, p90 %d, max %d (flat: %.1f)\n", mean,
+                 sc[sc.size() / 10], sc[sc.size() / 2], sc[sc.size() * 9 / 10], sc.back(), ncu * ph[2] / tot);
+        }
       }
   for (size_t v = 0; v < kos.size(); ++v)
     printf("%s%s%-6s N=%d T=%d H=%d W=%d Cin=%d Cout=%d ko=%-3d  %8.3f ms  %7.1f TF(alg)\n", p.res ? "res   " : "nores ", bf ? "bf16 " : "",
