@@ -715,6 +715,27 @@ def test_decoder_16row_tiles_bitexact(model, shape):
     assert torch.equal(s16, s8) and torch.equal(m16, m8)
 
 
+@pytest.mark.parametrize("dtype,variants", [
+    ("fp32", "w4r_cached_stores+winot_nt_stores+dma_nt_stores"),
+    ("bf16", "patch32_cached_stores+patch_nt_stores"),
+])
+def test_store_cache_policy_variants_bitexact(dtype, variants):
+    """Round 5's output-store cache policies (csrc: __builtin_nontemporal_store in conv_wino4r and
+    conv_patch32_bf16, the product; the cached / non-temporal alternatives in conv_winot5, conv_dma_x3
+    and conv_patch_bf16 as variants): only the stores' cache hint differs, so the forward is
+    bit-identical with every alternative switched at once."""
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    rng = np.random.default_rng(67)
+    x = torch.from_numpy(rng.uniform(0, 1, (2, 3, 32, 112, 112)).astype(np.float32)).cuda()
+    m = R2plus1D_18_MotionNet(pretrained=False, dtype=dtype)
+    s0, m0 = m(x)
+    m.set_kernel_variants(*variants.split("+"))
+    s1, m1 = m(x)
+    m.set_kernel_variants()
+    assert torch.isfinite(s0).all()
+    assert torch.equal(s0, s1) and torch.equal(m0, m1)
+
+
 @pytest.mark.parametrize("variant", ["no_dma_x3", "no_stem_x3"])
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (3, 3, 8, 32, 48)])
 def test_x3_convs_match_fp32_mfma(model, shape, variant):
