@@ -174,7 +174,11 @@ struct DmaDivs {
   FastDiv wo, ho, to, nt;
 };
 
-template <typename T, int MT, int NT, int S>
+// BUF (round 5, the bf16 engines' strided / 1x1x1 convs and projections): conv_dma_x3's buffer-offset
+// DMAs (a row's tap-validity bits and first-tap byte offset once per block; an A DMA is a bit test and
+// a select beside a scalar tap / channel offset, a B DMA a constant offset; out-of-range offsets read
+// zeros), where dma_buf_ok holds
+template <typename T, int MT, int NT, int S, bool BUF = false>
 __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDivs dv) {
   constexpr int EPS = 16 / sizeof(T);  // elements per 16-B slot
   constexpr int BKE = 4 * EPS;         // K elements per step (one 64-B row)
@@ -234,6 +238,42 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
   const int khw = p.KH * p.KW;
   const int kmain = p.KT * khw * p.Cin;  // K columns from x; the rest (1x1 dual input) from x2
 
+  // BUF: per A row the tap-validity bits and the byte offsets of its first tap's pixel (from x - padpix
+  // pixels, so never negative for a valid tap) in x and x2, slot dq included; per B slot the byte
+  // offset of its weight row
+  constexpr unsigned ES = sizeof(T);
+  unsigned a_vm[A_PER], a_bo[A_PER], a_bo2[A_PER], b_bo[PER_WAVE];
+  const int padpix = (p.pt * p.Hi + p.ph) * p.Wi + p.pw;
+  const size_t vox = (size_t)p.N * p.Ti * p.Hi * p.Wi;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      BUF ? const_cast<T*>(x - (size_t)padpix * p.Cin) : nullptr, (short)0, BUF ? (int)((vox + padpix) * p.Cin * ES) : 0,
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t x2r = __builtin_amdgcn_make_buffer_rsrc(
+      BUF && x2 ? const_cast<T*>(x2) : nullptr, (short)0, BUF && x2 ? (int)(vox * p.Cin2 * ES) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      BUF ? const_cast<T*>(w) : nullptr, (short)0, BUF ? (int)((size_t)p.Cout * p.Kp * ES) : 0, 0x00020000);
+  if constexpr (BUF) {
+#pragma unroll
+    for (int j = 0; j < A_PER; ++j) {
+      unsigned vm = 0;
+      for (int kt = 0; kt < p.KT; ++kt)
+        for (int kh = 0; kh < p.KH; ++kh)
+          for (int kw = 0; kw < p.KW; ++kw) {
+            const int ti = d_t[j] + kt, hi = d_h[j] + kh, wi = d_w[j] + kw;
+            const bool ok = ((unsigned)ti < (unsigned)p.Ti) & ((unsigned)hi < (unsigned)p.Hi) & ((unsigned)wi < (unsigned)p.Wi);
+            vm |= (ok ? 1u : 0u) << ((kt * p.KH + kh) * p.KW + kw);
+          }
+      a_vm[j] = vm;
+      a_bo[j] = (unsigned)(d_pix[j] + padpix) * (unsigned)(p.Cin * ES) + 16u * (unsigned)dq;
+      a_bo2[j] = (unsigned)d_pix[j] * (unsigned)(p.Cin2 * ES) + 16u * (unsigned)dq;
+    }
+#pragma unroll
+    for (int j = A_PER; j < PER_WAVE; ++j) {
+      const int idx = A_INS + wid + 4 * (j - A_PER);
+      b_bo[j] = idx < T_INS ? (unsigned)(((size_t)(n0 + (idx - A_INS) * 16 + drow) * p.Kp + EPS * dq) * ES) : 0x80000000u;
+    }
+  }
+
   // split-K (p.n_split > 1): this block sums K steps [kb, ke) of its tile
   const int nk_all = p.Kp / BKE;
   const int kb = split * nk_all / n_split, ke = (split + 1) * nk_all / n_split;
@@ -275,6 +315,24 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
         }
       }
       c_tap_pix = (c_kt * p.Hi + c_kh) * p.Wi + c_kw;
+    }
+    if constexpr (BUF) {
+      const unsigned tap = (unsigned)((kt * p.KH + kh) * p.KW + kw);
+      const unsigned soff = (unsigned)(tap_pix * cin + c0) * ES, sb = (unsigned)k0 * ES;
+#pragma unroll
+      for (int j = 0; j < PER_WAVE; ++j) {
+        const int idx = j < A_PER ? wid * A_PER + j : A_INS + wid + 4 * (j - A_PER);
+        char* dst = (idx < T_INS) ? smem + slot * STAGE + idx * 1024 : smem + JUNK;
+        if (j < A_PER) {
+          const unsigned off = ((a_vm[j] >> tap) & 1u) ? (second ? a_bo2[j] : a_bo[j]) : 0x80000000u;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(second ? x2r : xr, (__attribute__((address_space(3))) void*)dst, 16,
+                                                   off, soff, 0, 0);
+        } else {
+          const unsigned bo = b_bo[j];  // (through a local: see conv_dma_x3)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)dst, 16, bo, sb, 0, 0);
+        }
+      }
+      return;
     }
     const T* xc = xb + c0 + EPS * dq;
 #pragma unroll
@@ -978,13 +1036,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   }
 }
 
+// conv_dma's buffer-offset DMAs (BUF): the input from padpix pixels before its start, the second input
+// and the weights below 2^31 bytes, the tap mask in 32 bits, and the bf16 engines only -- the fp32 form
+// of conv_dma is a variant / fallback path (CLASFV_VARIANT_NO_DMA_BUF: the pointer form everywhere)
+bool dma_buf_ok(const ConvParams& p, size_t es) {
+  if ((p.vflags & CLASFV_VARIANT_NO_DMA_BUF) || es != 2) return false;
+  const size_t lim = (size_t)1 << 31;
+  const size_t vox = (size_t)p.N * p.Ti * p.Hi * p.Wi;
+  const size_t padpix = ((size_t)p.pt * p.Hi + p.ph) * p.Wi + p.pw;
+  return p.KT * p.KH * p.KW <= 32 && (vox + padpix) * p.Cin * es < lim && (!p.x2 || vox * p.Cin2 * es < lim) &&
+         (size_t)p.Cout * p.Kp * es < lim;
+}
+
 template <typename T, int MT, int NT, int S>
 hipError_t launch_dma(const ConvParams& p, hipStream_t s) {
   constexpr int BM = 64 * MT, BN = 16 * NT;
   const int mt = (p.M + BM - 1) / BM, nt = (p.Cout + BN - 1) / BN;
   const DmaDivs dv{fast_div(p.Wo), fast_div(p.Ho), fast_div(p.To), fast_div(nt)};
   const int n_split = p.n_split > 1 ? p.n_split : 1;
-  hipLaunchKernelGGL((conv_dma<T, MT, NT, S>), dim3(mt * nt * n_split), dim3(256), 0, s, p, nt, dv);
+  if (dma_buf_ok(p, sizeof(T)))
+    hipLaunchKernelGGL((conv_dma<T, MT, NT, S, true>), dim3(mt * nt * n_split), dim3(256), 0, s, p, nt, dv);
+  else
+    hipLaunchKernelGGL((conv_dma<T, MT, NT, S>), dim3(mt * nt * n_split), dim3(256), 0, s, p, nt, dv);
   if (n_split > 1) return launch_split_sum(p, s);
   return hipGetLastError();
 }

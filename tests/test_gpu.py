@@ -736,6 +736,30 @@ def test_store_cache_policy_variants_bitexact(dtype, variants):
     assert torch.equal(s0, s1) and torch.equal(m0, m1)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (2, 3, 32, 112, 112), (3, 3, 8, 32, 48)])
+def test_buffer_dmas_bitexact(dtype, shape):
+    """Round 5's buffer-offset LDS-DMAs (csrc/conv.hip BUF: per-row tap-validity bits and 32-bit byte
+    offsets; out-of-range offsets read zeros) in conv_dma_x3 (fp32 engines) and conv_dma (bf16 engines:
+    strided / 1x1x1 convs and the decoder projections) against the 64-bit pointer form (variant
+    no_dma_buf): the same bytes land in LDS, so the forward is bit-identical -- padded taps, rows past
+    M and the dual-input projections included."""
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    rng = np.random.default_rng(71)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    m = R2plus1D_18_MotionNet(pretrained=False, dtype=dtype)
+    m.engine.set_kernel_timing(True)
+    s0, m0 = m(x)
+    kt = m.engine.kernel_timing()
+    m.engine.set_kernel_timing(False)
+    assert ("conv_dma_x3" if dtype == "fp32" else "conv_dma") in kt
+    m.set_kernel_variants("no_dma_buf")
+    s1, m1 = m(x)
+    m.set_kernel_variants()
+    assert torch.isfinite(s0).all()
+    assert torch.equal(s0, s1) and torch.equal(m0, m1)
+
+
 @pytest.mark.parametrize("variant", ["no_dma_x3", "no_stem_x3"])
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (1, 3, 32, 112, 112), (3, 3, 8, 32, 48)])
 def test_x3_convs_match_fp32_mfma(model, shape, variant):
