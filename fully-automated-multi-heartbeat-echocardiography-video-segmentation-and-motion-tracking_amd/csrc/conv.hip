@@ -178,7 +178,9 @@ struct DmaDivs {
 // DMAs (a row's tap-validity bits and first-tap byte offset once per block; an A DMA is a bit test and
 // a select beside a scalar tap / channel offset, a B DMA a constant offset; out-of-range offsets read
 // zeros), where dma_buf_ok holds
-template <typename T, int MT, int NT, int S, bool BUF = false>
+// KO (tools/convbench timing knock-outs, 0 in the product; results wrong otherwise): 4 no DMAs in the
+// loop, 8 no waits / barriers, 16 no MFMAs
+template <typename T, int MT, int NT, int S, bool BUF = false, int KO = 0>
 __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDivs dv) {
   constexpr int EPS = 16 / sizeof(T);  // elements per 16-B slot
   constexpr int BKE = 4 * EPS;         // K elements per step (one 64-B row)
@@ -373,17 +375,20 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
   for (int k = 0; k < nk; ++k) {
     // stage k landed (this wave's DMAs), then every wave's (barrier); everyone is also done with
     // stage k-1, whose slot is refilled below.
-    if (k + S - 2 < nk) {
-      if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else if constexpr (S == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 * PER_WAVE) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_WAVE) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr ((KO & 8) == 0) {
+      if (k + S - 2 < nk) {
+        if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if constexpr (S == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 * PER_WAVE) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER_WAVE) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (k + S - 1 < nk) issue(kb + k + S - 1, (k + S - 1) % S);
+    if constexpr ((KO & 4) == 0)
+      if (k + S - 1 < nk) issue(kb + k + S - 1, (k + S - 1) % S);
     const char* st = smem + (k % S) * STAGE;
     if constexpr (sizeof(T) == 4) {
       f32x4 a[MT], b[NT];
@@ -404,10 +409,17 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
       for (int i = 0; i < MT; ++i) a[i] = *reinterpret_cast<const bf16x8*>(st + a_off + i * 16 * 64);
 #pragma unroll
       for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(st + b_off + j * 16 * 64);
+      if constexpr ((KO & 16) != 0) {
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+        for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < NT; ++j) acc[i][j][0] += (float)a[i][j & 7] * (float)b[j][i & 7];
+      } else {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      }
     }
   }
   if (n_split > 1)
@@ -1121,6 +1133,41 @@ hipError_t launch_stem(const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifdef CLASFV_KNOCKOUTS
+// tools/convbench.hip (CB_BF16 direct convs, ko 7300 + KO): conv_dma<__bf16, 2, NT, 3> knock-outs with
+// the buffer DMAs (KO & 1: the pointer form)
+template <int NT, int KO>
+hipError_t dma_ko_t(const ConvParams& p, hipStream_t s) {
+  constexpr int BM = 128, BN = 16 * NT;
+  const int mt = (p.M + BM - 1) / BM, nt = (p.Cout + BN - 1) / BN;
+  const DmaDivs dv{fast_div(p.Wo), fast_div(p.Ho), fast_div(p.To), fast_div(nt)};
+  hipLaunchKernelGGL((conv_dma<__bf16, 2, NT, 3, (KO & 1) == 0, KO & ~1>), dim3(mt * nt), dim3(256), 0, s, p, nt, dv);
+  return hipGetLastError();
+}
+template <int NT>
+hipError_t dma_ko_n(const ConvParams& p, int ko, hipStream_t s) {
+  switch (ko) {
+    case 0: return dma_ko_t<NT, 0>(p, s);
+    case 1: return dma_ko_t<NT, 1>(p, s);
+    case 4: return dma_ko_t<NT, 4>(p, s);
+    case 8: return dma_ko_t<NT, 8>(p, s);
+    case 16: return dma_ko_t<NT, 16>(p, s);
+    case 12: return dma_ko_t<NT, 12>(p, s);
+    case 28: return dma_ko_t<NT, 28>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+hipError_t dma_bf16_ko(const ConvParams& p, int bn, int ko, hipStream_t s) {
+  if (!p.in_bf16 || p.n_split > 1) return hipErrorInvalidValue;
+  switch (bn) {
+    case 64: return dma_ko_n<4>(p, ko, s);
+    case 96: return dma_ko_n<6>(p, ko, s);
+    case 128: return dma_ko_n<8>(p, ko, s);
+  }
+  return hipErrorInvalidValue;
+}
+#endif
+
 template <typename T>
 hipError_t launch_typed(const ConvParams& p, int bn, hipStream_t s) {
   switch (bn) {
@@ -1235,6 +1282,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 }
 
 }  // namespace
+
+#ifdef CLASFV_KNOCKOUTS
+hipError_t launch_dma_bf16_ko(const ConvParams& p, int bn, int ko, hipStream_t s) { return dma_bf16_ko(p, bn, ko, s); }
+#endif
 
 // conv_proj_x3: fp32 1x1x1 stride-1 convs to 64 channels over K = Cin (+ Cin2) = 128, both inputs
 // multiples of 32 channels, channels-last in and out, no split-K (the decoder projections P01 and P2;

@@ -25,6 +25,7 @@ hipError_t launch_winor_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_dma_x3_cfg(const ConvParams& p, int mt, int nt, int S, hipStream_t s);
 hipError_t launch_dma_x3_ko(const ConvParams& p, int nt, int ko, hipStream_t s);
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko);
+hipError_t launch_dma_bf16_ko(const ConvParams& p, int bn, int ko, hipStream_t s);
 hipError_t launch_patch_bf16_v1(const ConvParams& p, hipStream_t s);
 hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_patch32_bf16_epi(const ConvParams& p, hipStream_t s, int epi);
@@ -197,6 +198,10 @@ int main(int argc, char** argv) {
       if (getenv("CB_MT")) mt = atoi(getenv("CB_MT"));
       ConvParams q = p;
       if (ko >= 700 && ko < 709) q.n_split = ko - 700;  // conv_dma split-K into ko - 700 K ranges
+      if (bf && ko >= 7300 && ko < 7332) {  // conv_dma bf16 knock-outs (KO = ko - 7300; + 1 the pointer DMAs)
+        CK(launch_dma_bf16_ko(q, bn, ko - 7300, s));
+        return;
+      }
       if (ko >= 7200 && ko < 7264) {  // conv_dma_x3 knock-outs (KO = ko - 7200; + 32 the BUF form), N tile of CB_X3CFG's NT
         q.w = wx3;
         const char* cfg = getenv("CB_X3CFG");
