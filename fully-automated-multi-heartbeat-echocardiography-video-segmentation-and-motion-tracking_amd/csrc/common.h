@@ -146,6 +146,7 @@ bool stem_x3_supported(const ConvParams& p);
 hipError_t launch_stem_x3(const ConvParams& p, hipStream_t s);
 // conv_dma_x3: fp32 implicit GEMM on split-bf16 MFMAs (six products, fp32-accurate; conv.hip)
 bool dma_x3_supported(const ConvParams& p);
+bool dma_w_ok(const ConvParams& p);
 int dma_x3_bn(int cout_p);
 hipError_t launch_dma_x3(const ConvParams& p, int bn, hipStream_t s);
 void dma_x3_weight_image(const float* w, int cout_alloc, int Kp, uint16_t* out);

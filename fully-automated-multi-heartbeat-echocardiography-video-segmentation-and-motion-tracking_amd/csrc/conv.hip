@@ -429,6 +429,157 @@ __global__ __launch_bounds__(256) void conv_dma(ConvParams p, int n_tiles, DmaDi
 }
 
 // ---------------------------------------------------------------------------------------------
+// conv_dma_w (round 5, bf16 engines; Cin, Cin2 % 64 == 0): conv_dma<__bf16>'s implicit GEMM with
+// 128-B LDS rows -- a ring stage holds two 32-deep K steps of each A / B row side by side, so every
+// DMA row is a whole 128-B line of a tap's channels (conv_dma gathers 64-B half lines, and its
+// strided convs are bound by that gather: profiles/r05aj_bf16_conv_dma_buffer_dmas.txt). A DMA
+// instruction fills 8 rows (lane = row lane / 8, physical slot lane % 8, which holds logical slot
+// phys ^ (row % 8): 8 consecutive lanes of a fragment read hit distinct banks). The buffer-offset
+// DMAs of conv_dma's BUF form. Per stage the two K steps run in conv_dma's order (step 2s for
+// every (i, j), then step 2s + 1), so the outputs are bit-identical to conv_dma's.
+template <int MT, int NT, int S>
+__global__ __launch_bounds__(256) void conv_dma_w(ConvParams p, int n_tiles, DmaDivs dv) {
+  constexpr int BKE = 64;  // bf16 K elements per ring stage (one 128-B row)
+  constexpr int BM = 64 * MT, BN = 16 * NT;
+  constexpr int A_INS = BM / 8, B_INS = BN / 8, T_INS = A_INS + B_INS;  // DMA instructions (8 rows x 128 B)
+  constexpr int A_PER = A_INS / 4, B_PER = (B_INS + 3) / 4;
+  constexpr int PER_WAVE = A_PER + B_PER;
+  static_assert(A_INS % 4 == 0, "A rows split evenly over the 4 waves");
+  constexpr int STAGE = T_INS * 1024;
+  constexpr int JUNK = S * STAGE;
+  __shared__ __align__(16) char smem[S * STAGE + 1024];
+
+  const __bf16* x = reinterpret_cast<const __bf16*>(p.x);
+  const __bf16* x2 = reinterpret_cast<const __bf16*>(p.x2);
+  const __bf16* w = reinterpret_cast<const __bf16*>(p.w);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tile = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int tq = fdiv(tile, dv.nt);
+  const int m0 = tq * BM, n0 = (tile - tq * n_tiles) * BN;
+  const int q = lane >> 4, l16 = lane & 15;
+
+  const int drow = lane >> 3;               // row of the instruction's 8
+  const int dq = (lane & 7) ^ drow;         // logical 16-B slot this lane fetches (row % 8 = drow)
+  constexpr unsigned ES = 2;
+  const int padpix = (p.pt * p.Hi + p.ph) * p.Wi + p.pw;
+  const size_t vox = (size_t)p.N * p.Ti * p.Hi * p.Wi;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<__bf16*>(x - (size_t)padpix * p.Cin), (short)0, (int)((vox + padpix) * p.Cin * ES), 0x00020000);
+  const __amdgpu_buffer_rsrc_t x2r = __builtin_amdgcn_make_buffer_rsrc(
+      x2 ? const_cast<__bf16*>(x2) : nullptr, (short)0, x2 ? (int)(vox * p.Cin2 * ES) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(w), (short)0, (int)((size_t)p.Cout * p.Kp * ES), 0x00020000);
+  unsigned a_vm[A_PER], a_bo[A_PER], a_bo2[A_PER], b_bo[B_PER];
+#pragma unroll
+  for (int j = 0; j < A_PER; ++j) {
+    int m = m0 + (wid * A_PER + j) * 8 + drow;
+    const bool ok = m < p.M;
+    if (!ok) m = 0;
+    const int mw = fdiv(m, dv.wo), wo = m - mw * p.Wo;
+    const int mh = fdiv(mw, dv.ho), ho = mw - mh * p.Ho;
+    const int mt = fdiv(mh, dv.to), to = mh - mt * p.To;
+    const int dt = ok ? to * p.st - p.pt : -(1 << 20), dh = ho * p.sh - p.ph, dw = wo * p.sw - p.pw;
+    const int dpix = ((mt * p.Ti + dt) * p.Hi + dh) * p.Wi + dw;
+    unsigned vm = 0;
+    for (int kt = 0; kt < p.KT; ++kt)
+      for (int kh = 0; kh < p.KH; ++kh)
+        for (int kw = 0; kw < p.KW; ++kw) {
+          const int ti = dt + kt, hi = dh + kh, wi = dw + kw;
+          const bool v = ((unsigned)ti < (unsigned)p.Ti) & ((unsigned)hi < (unsigned)p.Hi) & ((unsigned)wi < (unsigned)p.Wi);
+          vm |= (v ? 1u : 0u) << ((kt * p.KH + kh) * p.KW + kw);
+        }
+    a_vm[j] = vm;
+    a_bo[j] = (unsigned)(dpix + padpix) * (unsigned)(p.Cin * ES) + 16u * (unsigned)dq;
+    a_bo2[j] = (unsigned)dpix * (unsigned)(p.Cin2 * ES) + 16u * (unsigned)dq;
+  }
+#pragma unroll
+  for (int j = 0; j < B_PER; ++j) {
+    const int idx = wid + 4 * j;  // B instruction: rows 8 idx .. 8 idx + 7 of the N tile
+    b_bo[j] = idx < B_INS ? (unsigned)(((size_t)(n0 + idx * 8 + drow) * p.Kp + 8 * dq) * ES) : 0x80000000u;
+  }
+  const int khw = p.KH * p.KW;
+  const int kmain = p.KT * khw * p.Cin;
+  int c_c0 = 0, c_kt = 0, c_kh = 0, c_kw = 0, c_tap_pix = 0;
+  bool c_second = kmain == 0;
+  auto issue = [&](int k_step, int slot) {
+    const bool second = c_second;
+    const int cin = second ? p.Cin2 : p.Cin;
+    const int c0 = c_c0, kt = c_kt, kh = c_kh, kw = c_kw, tap_pix = c_tap_pix;
+    c_c0 += BKE;
+    if (c_c0 == cin) {
+      c_c0 = 0;
+      if (++c_kw == p.KW) {
+        c_kw = 0;
+        if (++c_kh == p.KH) {
+          c_kh = 0;
+          if (++c_kt == p.KT) c_kt = 0, c_second = true;
+        }
+      }
+      c_tap_pix = (c_kt * p.Hi + c_kh) * p.Wi + c_kw;
+    }
+    const unsigned tap = (unsigned)((kt * p.KH + kh) * p.KW + kw);
+    const unsigned soff = (unsigned)(tap_pix * cin + c0) * ES, sb = (unsigned)(k_step * BKE) * ES;
+    char* stg = smem + slot * STAGE;
+#pragma unroll
+    for (int j = 0; j < A_PER; ++j) {
+      const unsigned off = ((a_vm[j] >> tap) & 1u) ? (second ? a_bo2[j] : a_bo[j]) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(second ? x2r : xr,
+                                               (__attribute__((address_space(3))) void*)(stg + (wid * A_PER + j) * 1024), 16,
+                                               off, soff, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < B_PER; ++j) {
+      const int idx = wid + 4 * j;
+      char* dst = idx < B_INS ? stg + (A_INS + idx) * 1024 : smem + JUNK;
+      const unsigned bo = b_bo[j];  // (through a local: see conv_dma_x3)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)dst, 16, bo, sb, 0, 0);
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.Kp / BKE;
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s, s);
+  // fragment rows: A row wid 16 MT + 16 i + l16, B row 16 j + l16 (both = l16 mod 8); slot (4 h + q)
+  const int sw = l16 & 7;
+  const int a_off = (wid * 16 * MT + l16) * 128, b_off = A_INS * 1024 + l16 * 128;
+  for (int k = 0; k < nk; ++k) {
+    if (k + S - 2 < nk) {
+      if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 * PER_WAVE) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (k + S - 1 < nk) issue(k + S - 1, (k + S - 1) % S);
+    const char* st = smem + (k % S) * STAGE;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int so = ((4 * h + q) ^ sw) * 16;
+      bf16x8 a[MT], b[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a[i] = *reinterpret_cast<const bf16x8*>(st + a_off + i * 16 * 128 + so);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(st + b_off + j * 16 * 128 + so);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+    }
+  }
+  epilogue<MT, NT>(p, acc, m0 + wid * 16 * MT, n0, q, l16);
+}
+
+// ---------------------------------------------------------------------------------------------
 // conv_dma_x3: the fp32 implicit GEMM on v_mfma_f32_16x16x32_bf16 with 3-way split operands.
 // x = hi + mid + lo (each the bf16 of the remainder: fp32's 24 bits); the product is accumulated in
 // fp32 as lo.hi + hi.lo + mid.mid + mid.hi + hi.mid + hi.hi (smallest first; the dropped terms are
@@ -1060,12 +1211,31 @@ bool dma_buf_ok(const ConvParams& p, size_t es) {
          (size_t)p.Cout * p.Kp * es < lim;
 }
 
+// conv_dma_w (128-B rows): bf16, every K step inside one tap of one input (Cin, Cin2 % 64), one K
+// range, the buffer-DMA limits (CLASFV_VARIANT_NO_DMA_W: conv_dma)
+bool dma_w_ok_(const ConvParams& p) {
+  if (p.vflags & CLASFV_VARIANT_NO_DMA_W) return false;
+  if (!p.in_bf16 || p.stem || p.n_split > 1 || !dma_buf_ok(p, 2)) return false;
+  return p.Cin % 64 == 0 && (!p.x2 || p.Cin2 % 64 == 0) && p.Kp == p.K && p.Kp % 64 == 0;
+}
+
+template <int MT, int NT, int S>
+hipError_t launch_dma_w(const ConvParams& p, hipStream_t s) {
+  constexpr int BM = 64 * MT, BN = 16 * NT;
+  const int mt = (p.M + BM - 1) / BM, nt = (p.Cout + BN - 1) / BN;
+  const DmaDivs dv{fast_div(p.Wo), fast_div(p.Ho), fast_div(p.To), fast_div(nt)};
+  hipLaunchKernelGGL((conv_dma_w<MT, NT, S>), dim3(mt * nt), dim3(256), 0, s, p, nt, dv);
+  return hipGetLastError();
+}
+
 template <typename T, int MT, int NT, int S>
 hipError_t launch_dma(const ConvParams& p, hipStream_t s) {
   constexpr int BM = 64 * MT, BN = 16 * NT;
   const int mt = (p.M + BM - 1) / BM, nt = (p.Cout + BN - 1) / BN;
   const DmaDivs dv{fast_div(p.Wo), fast_div(p.Ho), fast_div(p.To), fast_div(nt)};
   const int n_split = p.n_split > 1 ? p.n_split : 1;
+  if constexpr (sizeof(T) == 2 && MT == 2)
+    if (dma_w_ok_(p)) return launch_dma_w<MT, NT, 2>(p, s);
   if (dma_buf_ok(p, sizeof(T)))
     hipLaunchKernelGGL((conv_dma<T, MT, NT, S, true>), dim3(mt * nt * n_split), dim3(256), 0, s, p, nt, dv);
   else
@@ -1158,6 +1328,15 @@ hipError_t dma_ko_n(const ConvParams& p, int ko, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 hipError_t dma_bf16_ko(const ConvParams& p, int bn, int ko, hipStream_t s) {
+  if (ko == 100 || ko == 101) {  // conv_dma_w, 2 / 3 ring stages
+    if (!dma_w_ok_(p)) return hipErrorInvalidValue;
+    switch (bn) {
+      case 64: return ko == 100 ? launch_dma_w<2, 4, 2>(p, s) : launch_dma_w<2, 4, 3>(p, s);
+      case 96: return ko == 100 ? launch_dma_w<2, 6, 2>(p, s) : launch_dma_w<2, 6, 3>(p, s);
+      case 128: return ko == 100 ? launch_dma_w<2, 8, 2>(p, s) : launch_dma_w<2, 8, 3>(p, s);
+    }
+    return hipErrorInvalidValue;
+  }
   if (!p.in_bf16 || p.n_split > 1) return hipErrorInvalidValue;
   switch (bn) {
     case 64: return dma_ko_n<4>(p, ko, s);
@@ -1282,6 +1461,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 }
 
 }  // namespace
+
+bool dma_w_ok(const ConvParams& p) { return dma_w_ok_(p); }
 
 #ifdef CLASFV_KNOCKOUTS
 hipError_t launch_dma_bf16_ko(const ConvParams& p, int bn, int ko, hipStream_t s) { return dma_bf16_ko(p, bn, ko, s); }

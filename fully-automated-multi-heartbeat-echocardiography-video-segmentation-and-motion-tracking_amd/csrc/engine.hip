@@ -131,6 +131,7 @@ int env_variants() {
   if (on("CLASFV_DMA_NT_STORES")) f |= CLASFV_VARIANT_DMA_NT_STORES;
   if (on("CLASFV_PATCH32_CACHED_STORES")) f |= CLASFV_VARIANT_PATCH32_CACHED_STORES;
   if (on("CLASFV_PATCH_NT_STORES")) f |= CLASFV_VARIANT_PATCH_NT_STORES;
+  if (on("CLASFV_NO_DMA_W")) f |= CLASFV_VARIANT_NO_DMA_W;
   return f;
 }
 
@@ -438,7 +439,9 @@ const char* pick_kernel(const Conv& c, ConvParams p) {
     return "conv_patch32_bf16";
   if (!(p.vflags & CLASFV_VARIANT_NO_PATCH_BF16) && patch_bf16_supported(p)) return "conv_patch_bf16";
   if (c.dx3 && dma_x3_supported(p)) return "conv_dma_x3";
-  return c.stem ? "conv_stem_f32" : "conv_dma";
+  if (c.stem) return "conv_stem_f32";
+  // bf16 direct convs with whole 128-B tap rows (launch_dma takes conv_dma_w at the 128-row M tile)
+  return dma_w_ok(p) ? "conv_dma_w" : "conv_dma";
 }
 
 // Whether the mid tensor between producer `a` (input shape `in`) and consumer `b` goes through HBM
@@ -898,7 +901,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0xFFFFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~0x1FFFFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;

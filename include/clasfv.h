@@ -84,7 +84,8 @@ enum {
   CLASFV_VARIANT_WINOT_NT_STORES = 1048576, /* CLASFV_WINOT_NT_STORES: conv_winot5's output stores non-temporal (A/B) */
   CLASFV_VARIANT_DMA_NT_STORES = 2097152,   /* CLASFV_DMA_NT_STORES: conv_dma_x3's output stores non-temporal (A/B) */
   CLASFV_VARIANT_PATCH32_CACHED_STORES = 4194304, /* CLASFV_PATCH32_CACHED_STORES: conv_patch32_bf16's output stores cached (the product's are non-temporal) */
-  CLASFV_VARIANT_PATCH_NT_STORES = 8388608  /* CLASFV_PATCH_NT_STORES: conv_patch_bf16's output stores non-temporal (A/B) */
+  CLASFV_VARIANT_PATCH_NT_STORES = 8388608, /* CLASFV_PATCH_NT_STORES: conv_patch_bf16's output stores non-temporal (A/B) */
+  CLASFV_VARIANT_NO_DMA_W = 16777216        /* CLASFV_NO_DMA_W: the bf16 engines' direct convs on conv_dma (64-B rows) instead of conv_dma_w (128-B rows) */
 };
 
 typedef struct clasfv_engine* clasfv_t;

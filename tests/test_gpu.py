@@ -752,8 +752,30 @@ def test_buffer_dmas_bitexact(dtype, shape):
     s0, m0 = m(x)
     kt = m.engine.kernel_timing()
     m.engine.set_kernel_timing(False)
-    assert ("conv_dma_x3" if dtype == "fp32" else "conv_dma") in kt
+    assert ("conv_dma_x3" in kt) if dtype == "fp32" else ("conv_dma" in kt or "conv_dma_w" in kt)
     m.set_kernel_variants("no_dma_buf")
+    s1, m1 = m(x)
+    m.set_kernel_variants()
+    assert torch.isfinite(s0).all()
+    assert torch.equal(s0, s1) and torch.equal(m0, m1)
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (2, 3, 32, 112, 112), (3, 3, 8, 32, 48)])
+def test_bf16_dma_w_bitexact(shape):
+    """The bf16 engines' direct convs on conv_dma_w (csrc/conv.hip: 128-B LDS rows, two 32-deep K steps
+    per ring stage, every DMA row a whole line of a tap's channels) against conv_dma (64-B rows; variant
+    no_dma_w): the same bf16 products accumulated in the same order, so the forward is bit-identical
+    (convbench CB_CHECK on layer2 / layer3 strided convs: profiles/r05ao_conv_dma_w.txt)."""
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    rng = np.random.default_rng(73)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    m = R2plus1D_18_MotionNet(pretrained=False, dtype="bf16")
+    m.engine.set_kernel_timing(True)
+    s0, m0 = m(x)
+    kt = m.engine.kernel_timing()
+    m.engine.set_kernel_timing(False)
+    assert "conv_dma_w" in kt
+    m.set_kernel_variants("no_dma_w")
     s1, m1 = m(x)
     m.set_kernel_variants()
     assert torch.isfinite(s0).all()

@@ -198,7 +198,7 @@ int main(int argc, char** argv) {
       if (getenv("CB_MT")) mt = atoi(getenv("CB_MT"));
       ConvParams q = p;
       if (ko >= 700 && ko < 709) q.n_split = ko - 700;  // conv_dma split-K into ko - 700 K ranges
-      if (bf && ko >= 7300 && ko < 7332) {  // conv_dma bf16 knock-outs (KO = ko - 7300; + 1 the pointer DMAs)
+      if (bf && ko >= 7300 && ko < 7402) {  // conv_dma bf16 knock-outs (KO = ko - 7300; + 1 the pointer DMAs); 7400 / 7401: conv_dma_w, 2 / 3 stages
         CK(launch_dma_bf16_ko(q, bn, ko - 7300, s));
         return;
       }
