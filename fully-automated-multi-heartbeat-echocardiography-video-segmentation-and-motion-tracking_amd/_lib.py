@@ -54,7 +54,8 @@ VARIANTS = {"no_winograd": 1, "no_wino_patch": 2, "winot_reference": 4, "no_c8":
             "decoder_rows16": 131072, "no_dma_buf": 262144,
             "w4r_cached_stores": 524288, "winot_nt_stores": 1048576,
             "dma_nt_stores": 2097152, "patch32_cached_stores": 4194304,
-            "patch_nt_stores": 8388608, "no_dma_w": 16777216}
+            "patch_nt_stores": 8388608, "no_dma_w": 16777216,
+            "dma_x3_wr": 33554432}
 DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
 _lib = None
 

@@ -604,8 +604,13 @@ __global__ __launch_bounds__(256) void conv_dma_w(ConvParams p, int n_tiles, Dma
 // KO (tools/convbench timing knock-outs, 0 in the product; results wrong otherwise): 1 no activation
 // split (the fp32 bits reinterpreted as the three pieces), 2 no B-piece LDS reads, 4 no DMAs in the
 // loop, 8 no waits / barriers, 16 no epilogue.
-template <int MT, int NT, int S, int WN = 1, int EF = -1, int KO = 0, bool BUF = false, bool NTS = false>
+// WR (round 5, with BUF; Cin, Cin2 % 32 == 0 and an even step count): conv_dma_w's 128-B A rows -- a
+// pixel's 32 channels of the pair in one LDS row (slots 0-3 the first step, 4-7 the second, XOR-swizzled
+// by row % 8), so every A DMA row is a whole line; B, the products and their order are unchanged
+// (bit-identical).
+template <int MT, int NT, int S, int WN = 1, int EF = -1, int KO = 0, bool BUF = false, bool NTS = false, bool WR = false>
 __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, DmaDivs dv) {
+  static_assert(!WR || BUF, "128-B A rows use the buffer DMAs");
   static_assert(NT % WN == 0, "N tiles split evenly over the waves along N");
   constexpr int MTW = MT * WN, NTW = NT / WN;  // 16 x 16 tiles per wave
   constexpr int BM = 64 * MT, BN = 16 * NT;
@@ -638,10 +643,13 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
   const int npairs = (nsteps + 1) / 2;    // ring stages; an odd last step pairs with zeros
   const int drow = lane >> 2;
   const int dq = (lane & 3) ^ G[(drow >> 2) & 3];
-  int d_t[A_PER], d_h[A_PER], d_w[A_PER], d_pix[A_PER];
+  // A rows per lane: WR: 2 A_PER rows of 8 per instruction (row lane / 8), else A_PER rows of 16
+  constexpr int RA = WR ? 2 * A_PER : A_PER;
+  const int adq = WR ? (lane & 7) ^ (lane >> 3) : dq;  // logical A slot this lane fetches
+  int d_t[RA], d_h[RA], d_w[RA], d_pix[RA];
 #pragma unroll
-  for (int j = 0; j < A_PER; ++j) {
-    int m = m0 + (wid * A_PER + j) * 16 + drow;
+  for (int j = 0; j < RA; ++j) {
+    int m = WR ? m0 + (wid * RA + j) * 8 + (lane >> 3) : m0 + (wid * A_PER + j) * 16 + drow;
     const bool ok = m < p.M;
     if (!ok) m = 0;
     const int mw = fdiv(m, dv.wo), wo = m - mw * p.Wo;
@@ -665,7 +673,7 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
   }
   // BUF: per A row, the tap-validity bits (tap = (kt KH + kh) KW + kw; 0 for a row past M) and the
   // byte offsets of its first tap's pixel in x and x2 (16-B slot dq included)
-  unsigned a_vm[A_PER], a_bo[A_PER], a_bo2[A_PER];
+  unsigned a_vm[RA], a_bo[RA], a_bo2[RA];
   const int padpix = (p.pt * p.Hi + p.ph) * p.Wi + p.pw;  // the most negative first-tap pixel of a row
   const size_t vox = (size_t)p.N * p.Ti * p.Hi * p.Wi;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
@@ -677,7 +685,7 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
       BUF ? const_cast<__bf16*>(w) : nullptr, (short)0, BUF ? (int)((size_t)p.Cout * npairs * 192) : 0, 0x00020000);
   if constexpr (BUF) {
 #pragma unroll
-    for (int j = 0; j < A_PER; ++j) {
+    for (int j = 0; j < RA; ++j) {
       unsigned vm = 0;
       for (int kt = 0; kt < p.KT; ++kt)
         for (int kh = 0; kh < p.KH; ++kh)
@@ -688,8 +696,8 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
           }
       a_vm[j] = vm;
       // offsets from x - padpix pixels: never negative for a valid tap, so neither buffer offset wraps
-      a_bo[j] = (unsigned)(d_pix[j] + padpix) * (unsigned)(p.Cin * 4) + 16u * (unsigned)dq;
-      a_bo2[j] = (unsigned)d_pix[j] * (unsigned)(p.Cin2 * 4) + 16u * (unsigned)dq;
+      a_bo[j] = (unsigned)(d_pix[j] + padpix) * (unsigned)(p.Cin * 4) + 16u * (unsigned)adq;
+      a_bo2[j] = (unsigned)d_pix[j] * (unsigned)(p.Cin2 * 4) + 16u * (unsigned)adq;
     }
   }
   const int khw = p.KH * p.KW;
@@ -714,8 +722,34 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
   }
   auto issue = [&](int pair, int slot) {
     char* stg = smem + slot * STAGE;
+    if constexpr (WR) {
+      // both steps of the pair inside one tap of one input (Cin, Cin2 % 32): one cursor step of 32
+      const bool second = c_second;
+      const int cin = second ? p.Cin2 : p.Cin;
+      const int c0 = c_c0, kt = c_kt, kh = c_kh, kw = c_kw, tap_pix = c_tap_pix;
+      c_c0 += 32;
+      if (c_c0 == cin) {
+        c_c0 = 0;
+        if (++c_kw == p.KW) {
+          c_kw = 0;
+          if (++c_kh == p.KH) {
+            c_kh = 0;
+            if (++c_kt == p.KT) c_kt = 0, c_second = true;
+          }
+        }
+        c_tap_pix = (c_kt * p.Hi + c_kh) * p.Wi + c_kw;
+      }
+      const unsigned tap = (unsigned)((kt * p.KH + kh) * p.KW + kw);
+      const unsigned soff = (unsigned)(tap_pix * cin + c0) * 4u;
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
+      for (int j = 0; j < RA; ++j) {
+        const unsigned off = ((a_vm[j] >> tap) & 1u) ? (second ? a_bo2[j] : a_bo[j]) : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            second ? x2r : xr, (__attribute__((address_space(3))) void*)(stg + (wid * RA + j) * 1024), 16, off, soff, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int sub = 0; sub < (WR ? 0 : 2); ++sub) {
       const bool valid = 2 * pair + sub < nsteps;  // wave-uniform
       const bool second = c_second;
       const int cin = second ? p.Cin2 : p.Cin;
@@ -812,8 +846,15 @@ __global__ __launch_bounds__(256) void conv_dma_x3(ConvParams p, int n_tiles, Dm
     bf16x8 ah[MTW], am[MTW], al[MTW];
 #pragma unroll
     for (int i = 0; i < MTW; ++i) {
-      const f32x4 a0 = *reinterpret_cast<const f32x4*>(st + a_off + i * 16 * 64);
-      const f32x4 a1 = *reinterpret_cast<const f32x4*>(st + A_BYTES + a_off + i * 16 * 64);
+      f32x4 a0, a1;
+      if constexpr (WR) {
+        const char* ar = st + (wm * 16 * MTW + i * 16 + l16) * 128;
+        a0 = *reinterpret_cast<const f32x4*>(ar + ((q ^ (l16 & 7)) * 16));
+        a1 = *reinterpret_cast<const f32x4*>(ar + (((4 + q) ^ (l16 & 7)) * 16));
+      } else {
+        a0 = *reinterpret_cast<const f32x4*>(st + a_off + i * 16 * 64);
+        a1 = *reinterpret_cast<const f32x4*>(st + A_BYTES + a_off + i * 16 * 64);
+      }
       if constexpr ((KO & 1) != 0) {
         ah[i] = __builtin_bit_cast(bf16x8, a0);
         am[i] = __builtin_bit_cast(bf16x8, a1);
@@ -1272,6 +1313,26 @@ hipError_t launch_dma_x3_t(const ConvParams& p, hipStream_t s) {
       hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 2, 0, true, true>), grid, dim3(256), 0, s, p, nt, dv);
     else
       hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 3, 0, true, true>), grid, dim3(256), 0, s, p, nt, dv);
+    return hipGetLastError();
+  }
+  // 128-B A rows (WR) where both steps of every pair share a tap: a variant (CLASFV_VARIANT_DMA_X3_WR).
+  // Bit-identical, but the forward's conv_dma_x3 time went 4.31 -> 4.37 ms per step (three A/B pairs,
+  // profiles/r05aq_dma_x3_wide_rows.txt): unlike the bf16 conv_dma, the split-bf16 loop is not
+  // gather-bound enough for whole-line rows to pay for the doubled per-lane row state
+  const bool wr = dma_x3_buf_ok(p, nt * BN) && (p.vflags & CLASFV_VARIANT_DMA_X3_WR) && p.Cin % 32 == 0 &&
+                  (!p.x2 || p.Cin2 % 32 == 0) && p.Kp % 32 == 0;
+  if (wr) {
+    switch (ef) {
+      case 0: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 0, 0, true, false, true>), grid, dim3(256), 0, s, p, nt, dv); break;
+      case 1: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 1, 0, true, false, true>), grid, dim3(256), 0, s, p, nt, dv); break;
+      case 2: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 2, 0, true, false, true>), grid, dim3(256), 0, s, p, nt, dv); break;
+      case 3: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 3, 0, true, false, true>), grid, dim3(256), 0, s, p, nt, dv); break;
+      default:
+        if (ef >= 8 || ef < 4) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, -1, 0, true, false, true>), grid, dim3(256), 0, s, p, nt, dv);
+        break;
+    }
+    if (n_split > 1) return launch_split_sum(p, s);
     return hipGetLastError();
   }
   switch (dma_x3_buf_ok(p, nt * BN) ? ef + 8 : ef) {

@@ -132,6 +132,7 @@ int env_variants() {
   if (on("CLASFV_PATCH32_CACHED_STORES")) f |= CLASFV_VARIANT_PATCH32_CACHED_STORES;
   if (on("CLASFV_PATCH_NT_STORES")) f |= CLASFV_VARIANT_PATCH_NT_STORES;
   if (on("CLASFV_NO_DMA_W")) f |= CLASFV_VARIANT_NO_DMA_W;
+  if (on("CLASFV_DMA_X3_WR")) f |= CLASFV_VARIANT_DMA_X3_WR;
   return f;
 }
 
@@ -901,7 +902,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0x1FFFFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~0x3FFFFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;

@@ -85,7 +85,8 @@ enum {
   CLASFV_VARIANT_DMA_NT_STORES = 2097152,   /* CLASFV_DMA_NT_STORES: conv_dma_x3's output stores non-temporal (A/B) */
   CLASFV_VARIANT_PATCH32_CACHED_STORES = 4194304, /* CLASFV_PATCH32_CACHED_STORES: conv_patch32_bf16's output stores cached (the product's are non-temporal) */
   CLASFV_VARIANT_PATCH_NT_STORES = 8388608, /* CLASFV_PATCH_NT_STORES: conv_patch_bf16's output stores non-temporal (A/B) */
-  CLASFV_VARIANT_NO_DMA_W = 16777216        /* CLASFV_NO_DMA_W: the bf16 engines' direct convs on conv_dma (64-B rows) instead of conv_dma_w (128-B rows) */
+  CLASFV_VARIANT_NO_DMA_W = 16777216,       /* CLASFV_NO_DMA_W: the bf16 engines' direct convs on conv_dma (64-B LDS rows) instead of conv_dma_w (128-B rows) */
+  CLASFV_VARIANT_DMA_X3_WR = 33554432       /* CLASFV_DMA_X3_WR: conv_dma_x3 with 128-B A rows (A/B; slower) */
 };
 
 typedef struct clasfv_engine* clasfv_t;

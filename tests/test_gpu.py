@@ -760,6 +760,20 @@ def test_buffer_dmas_bitexact(dtype, shape):
     assert torch.equal(s0, s1) and torch.equal(m0, m1)
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (3, 3, 8, 32, 48)])
+def test_dma_x3_wide_rows_bitexact(model, shape):
+    """conv_dma_x3 with 128-B A rows (variant dma_x3_wr: both 16-channel steps of a K pair in one LDS
+    row, whole-line tap DMAs) against the product's 64-B rows: the same fp32 bytes reach the split and
+    the same products run in the same order, so the fp32 forward is bit-identical."""
+    rng = np.random.default_rng(79)
+    x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
+    s0, m0 = model(x)
+    model.set_kernel_variants("dma_x3_wr")
+    s1, m1 = model(x)
+    model.set_kernel_variants()
+    assert torch.equal(s0, s1) and torch.equal(m0, m1)
+
+
 @pytest.mark.parametrize("shape", [(2, 3, 16, 64, 96), (2, 3, 32, 112, 112), (3, 3, 8, 32, 48)])
 def test_bf16_dma_w_bitexact(shape):
     """The bf16 engines' direct convs on conv_dma_w (csrc/conv.hip: 128-B LDS rows, two 32-deep K steps
