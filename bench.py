@@ -209,12 +209,16 @@ def kernel_table(kt, engine_dtype):
         out[k] = {"launches": v["launches"], "ms": round(v["ms"], 3), "pipe": pipe,
                   "issued_tflops": round(r, 2), "issued_frac_of_pipe_peak": round(r / PIPE_PEAK[pipe], 4),
                   "algorithmic_tflops": round(v["gflop"] / max(v["ms"], 1e-9), 2),
-                  "pmc_mfma_busy": b and b[0], "pmc_clock_ghz": b and b[1]}
-    return {"kernels": out, "pmc_source": src,
+                  "committed_pmc_mfma_busy": b and b[0], "committed_pmc_clock_ghz": b and b[1]}
+    return {"kernels": out, "committed_pmc_source": src,
             "note": "issued = products the kernel issues to the matrix pipe it runs on (f32: 157.3 TFLOP/s; "
-                    "bf16: 2.5 PFLOP/s dense; split-bf16 x3 kernels: 6 bf16 products per fp32 product) / its "
-                    "summed HIP-event time; pmc_mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (cycles x 1,024 SIMDs) "
-                    "from the committed profile pmc_source (null: kernel not in it)"}
+                    "bf16: 2.5 PFLOP/s dense; split-bf16 x3 kernels: 6 bf16 products per fp32 product since "
+                    "round 5 -- earlier rounds' bench lines counted them as fp32 products, so their "
+                    "issued_tflops are not comparable) / its summed HIP-event time, THIS run; "
+                    "committed_pmc_mfma_busy / committed_pmc_clock_ghz = SQ_VALU_MFMA_BUSY_CYCLES / (cycles x "
+                    "1,024 SIMDs) and GRBM_GUI_ACTIVE / 8 / wall time from the committed PMC pass "
+                    "committed_pmc_source, profiled on the build that file's round tag names -- NOT measured "
+                    "in this run and possibly on older kernels (null: kernel not in it)"}
 
 
 def forward_stats(kt, clips, gflop_per_clip, peak, engine_dtype="fp32"):
@@ -477,6 +481,7 @@ def c2_measure(args, model, world, rank, dev, lengths, fuse, steps, warmup):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     fwd = forward_stats(kt, (hi - lo) * steps, GFLOP_PER_CLIP, peak, args.dtype)
     rows, nbytes = D.exchange_stats(lengths, fuse, args.step, world)
+    xfer_ms = exchange_transfer_ms(lengths, fuse, args.step, rank, world, dev) if rows else 0.0
     mine = {"rank": rank, "clips": hi - lo, "videos_held": len(needed), "videos_fused": len(out),
             "forward_ms_per_step": round(sum(v["ms"] for v in kt.values()) / steps, 3)}
     per_rank = gather_ranks(mine, world)
@@ -486,11 +491,39 @@ def c2_measure(args, model, world, rank, dev, lengths, fuse, steps, warmup):
             "clips_per_step": n_total, "fuse": fuse, "forward": fwd, "per_rank": per_rank,
             "rows_exchanged_per_step": rows, "bytes_exchanged_per_step": nbytes,
             "exchange_ms_per_step": round(float(t.item()), 4),
+            "exchange_transfer_ms": round(xfer_ms, 4),
             "exchange_note": "margin planes (fp32, 32 x 112 x 112 per crossing clip) through one all_to_all_single "
-                             "(RCCL over xGMI with nccl; host-staged with gloo); time = events on the compute stream "
-                             "around logit_margin + the collective, max over ranks (includes waiting for the "
-                             "slowest rank's forward)",
+                             "(RCCL over xGMI with nccl; host-staged with gloo). exchange_ms_per_step = events on the "
+                             "compute stream around logit_margin + the collective inside the timed steps, max over "
+                             "ranks: it includes waiting for the slowest rank's forward (skew); "
+                             "exchange_transfer_ms = the same all_to_all alone, every rank entering together "
+                             "(barrier + synchronize before it), median of 5, max over ranks: the transfer",
             "roofline": kernel_roofline(kt, peak, args.dtype), "kt": kt, "out": out}
+
+
+def exchange_transfer_ms(lengths, fuse, step, rank, world, dev, reps=5):
+    """The owner all_to_all of one sharded pass alone (same split sizes as the timed steps, zero margin
+    planes), with the ranks synchronised before each repetition so no forward skew is included:
+    median of `reps`, max over ranks."""
+    from clasfv_amd import dist as D
+    plans, n_total = D.global_clip_plan(lengths, fuse, step)
+    owners = D.owner_of_clips(plans, world)
+    lo, hi = D.shard_bounds(n_total, rank, world)
+    local = torch.zeros((hi - lo, 32, 112, 112), dtype=torch.float32, device=dev)
+    times = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        dist.barrier()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        D.exchange_to_owners(local, owners, rank, world)
+        b.record()
+        torch.cuda.synchronize()
+        times.append(a.elapsed_time(b))
+    t = torch.tensor([float(np.median(times[1:]))], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    del local
+    return float(t.item())
 
 
 def run_c2(args, model, world, rank, dev):

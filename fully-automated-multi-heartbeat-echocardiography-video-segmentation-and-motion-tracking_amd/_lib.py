@@ -51,11 +51,8 @@ VARIANTS = {"no_winograd": 1, "no_wino_patch": 2, "winot_reference": 4, "no_c8":
             "no_patch_bf16": 32, "no_decoder_bf16": 64, "winot_no_ts1": 128, "no_split_k": 256, "no_wino4": 512,
             "no_decoder_x3": 1024, "no_dma_x3": 2048, "no_stem_x3": 4096, "no_wino4w": 8192,
             "no_patch32": 16384, "no_proj_x3": 32768, "no_wino4r": 65536,
-            "decoder_rows16": 131072, "no_dma_buf": 262144,
-            "w4r_cached_stores": 524288, "winot_nt_stores": 1048576,
-            "dma_nt_stores": 2097152, "patch32_cached_stores": 4194304,
-            "patch_nt_stores": 8388608, "no_dma_w": 16777216,
-            "dma_x3_wr": 33554432}
+            "no_dma_buf": 262144, "w4r_cached_stores": 524288,
+            "patch32_cached_stores": 4194304, "no_dma_w": 16777216}
 DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
 _lib = None
 

@@ -94,7 +94,6 @@ struct DecParams {
   int N, T, H, W;
   int bf16;           // comb_2 on bf16 MFMAs (bf16 engines; taps, heads and outputs stay fp32)
   int x3;             // fp32 engines: comb_2 as six bf16 products of 3-way split operands (fp32-accurate)
-  int rows16;         // CLASFV_VARIANT_DECODER_ROWS16: the X3 decoder on 16-row tiles instead of 8
 };
 
 // Launchers (stream-ordered, no synchronisation). Return hipError_t of the launch.

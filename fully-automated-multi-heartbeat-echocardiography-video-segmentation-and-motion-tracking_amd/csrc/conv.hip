@@ -1308,33 +1308,10 @@ hipError_t launch_dma_x3_t(const ConvParams& p, hipStream_t s) {
   // the epilogue flags at compile time (split-K partials ignore them); the buffer-offset DMAs where
   // every tensor fits them
   const int ef = n_split > 1 ? 0 : (p.res ? 1 : 0) | (p.relu ? 2 : 0) | (p.y_c8 ? 4 : 0);
-  if ((p.vflags & CLASFV_VARIANT_DMA_NT_STORES) && n_split == 1 && dma_x3_buf_ok(p, nt * BN) && (ef == 2 || ef == 3)) {
-    if (ef == 2)
-      hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 2, 0, true, true>), grid, dim3(256), 0, s, p, nt, dv);
-    else
-      hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 3, 0, true, true>), grid, dim3(256), 0, s, p, nt, dv);
-    return hipGetLastError();
-  }
-  // 128-B A rows (WR) where both steps of every pair share a tap: a variant (CLASFV_VARIANT_DMA_X3_WR).
-  // Bit-identical, but the forward's conv_dma_x3 time went 4.31 -> 4.37 ms per step (three A/B pairs,
-  // profiles/r05aq_dma_x3_wide_rows.txt): unlike the bf16 conv_dma, the split-bf16 loop is not
-  // gather-bound enough for whole-line rows to pay for the doubled per-lane row state
-  const bool wr = dma_x3_buf_ok(p, nt * BN) && (p.vflags & CLASFV_VARIANT_DMA_X3_WR) && p.Cin % 32 == 0 &&
-                  (!p.x2 || p.Cin2 % 32 == 0) && p.Kp % 32 == 0;
-  if (wr) {
-    switch (ef) {
-      case 0: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 0, 0, true, false, true>), grid, dim3(256), 0, s, p, nt, dv); break;
-      case 1: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 1, 0, true, false, true>), grid, dim3(256), 0, s, p, nt, dv); break;
-      case 2: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 2, 0, true, false, true>), grid, dim3(256), 0, s, p, nt, dv); break;
-      case 3: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 3, 0, true, false, true>), grid, dim3(256), 0, s, p, nt, dv); break;
-      default:
-        if (ef >= 8 || ef < 4) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, -1, 0, true, false, true>), grid, dim3(256), 0, s, p, nt, dv);
-        break;
-    }
-    if (n_split > 1) return launch_split_sum(p, s);
-    return hipGetLastError();
-  }
+  // (round 5 A/B forms not in the library: non-temporal output stores ±0 in the forward,
+  // profiles/r05ac_nt_stores_ab2.txt; 128-B A rows, bit-identical but 4.31 -> 4.37 ms per forward,
+  // profiles/r05aq_dma_x3_wide_rows.txt -- the split-bf16 loop is not gather-bound enough for
+  // whole-line rows to pay for the doubled per-lane row state)
   switch (dma_x3_buf_ok(p, nt * BN) ? ef + 8 : ef) {
     case 0: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 0>), grid, dim3(256), 0, s, p, nt, dv); break;
     case 1: hipLaunchKernelGGL((conv_dma_x3<MT, NT, S, WN, 1>), grid, dim3(256), 0, s, p, nt, dv); break;
@@ -1421,8 +1398,10 @@ hipError_t launch_typed(const ConvParams& p, int bn, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-// bf16 with BM = 256 (4 waves x 64 rows): a K step moves (16 + NT) KiB for 16*NT MFMAs per wave
-// instead of (8 + NT) KiB for 8*NT -- the direct bf16 convs are bound by the global->LDS bytes.
+#ifdef CLASFV_KNOCKOUTS
+// (convbench CB_MT=4 only) bf16 with BM = 256 (4 waves x 64 rows): a K step moves (16 + NT) KiB for
+// 16*NT MFMAs per wave instead of (8 + NT) KiB for 8*NT; measured slower than conv_dma_w's BM 128
+// (0.48-0.50 vs 0.435 ms on layer2's strided conv, profiles/r05aj_bf16_conv_dma_buffer_dmas.txt)
 hipError_t launch_bf16_m4(const ConvParams& p, int bn, hipStream_t s) {
   switch (bn) {
     case 48: return launch_dma<__bf16, 4, 3, 3>(p, s);
@@ -1434,6 +1413,7 @@ hipError_t launch_bf16_m4(const ConvParams& p, int bn, hipStream_t s) {
   }
   return hipErrorInvalidValue;
 }
+#endif
 
 // fp32-engine stem on split-bf16 MFMAs (conv_stem_x3): conv_stem_bf16's structure and K order with
 // three bf16 pieces per operand (x = hi + mid + lo, fp32's 24 bits) and the six products of
@@ -1735,7 +1715,9 @@ int dma_split_for(const ConvParams& p, int mt) {
 }
 
 hipError_t launch_conv(const ConvParams& p, int mt, int bn, hipStream_t s) {
+#ifdef CLASFV_KNOCKOUTS
   if (mt == 4 && p.in_bf16 && !p.stem) return launch_bf16_m4(p, bn, s);
+#endif
   if (mt != 2) return hipErrorInvalidValue;
   if (p.stem) {  // fp32 input with 4 channels (3 + zero pad)
     if (bn == 48) return launch_stem<3>(p, s);

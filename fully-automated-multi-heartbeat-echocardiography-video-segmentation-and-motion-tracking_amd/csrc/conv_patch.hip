@@ -375,15 +375,6 @@ hipError_t launch_pe(const ConvParams& p, hipStream_t s) {
 
 template <int NT, int KT, int FR, int S = 3, bool STG = true>
 hipError_t launch_p(const ConvParams& p, hipStream_t s) {
-  if constexpr (STG) {
-    // EF 4: non-temporal output stores (A/B variant CLASFV_PATCH_NT_STORES)
-    if (p.vflags & CLASFV_VARIANT_PATCH_NT_STORES) switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
-      case 0: return launch_pe<NT, KT, FR, S, STG, 4>(p, s);
-      case 1: return launch_pe<NT, KT, FR, S, STG, 5>(p, s);
-      case 2: return launch_pe<NT, KT, FR, S, STG, 6>(p, s);
-      default: return launch_pe<NT, KT, FR, S, STG, 7>(p, s);
-    }
-  }
   switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
     case 0: return launch_pe<NT, KT, FR, S, STG, 0>(p, s);
     case 1: return launch_pe<NT, KT, FR, S, STG, 1>(p, s);
@@ -753,13 +744,15 @@ hipError_t launch_p32(const ConvParams& p, hipStream_t s) {
 }
 
 // N tile (32-channel blocks). Product rule: NB = 5 (160-channel blocks: the bf16 layer1 spatial
-// convs, 64 -> 160) on grids of >= 512 blocks; everywhere else conv_patch_bf16 is as fast or faster
-// (convbench, profiles/r04_patch32_bf16.txt: layer1 0.686 vs 0.726 ms, layer2 288 channels at NB 3
-// 0.325 vs 0.313, layer3 576 at NB 3 0.152 vs 0.156, layer4 1152 at NB 2 0.114 vs 0.088). 0: not
-// taken. force_nb > 0 (convbench, CLASFV_PATCH_NT = -NB) takes any NB that divides.
-// The size rule counts blocks PER CLIP (>= 128: every 112x112-clip layer1 map; 32x112x112 gives 392),
-// never the batch's, so whether a clip's layer1 runs 32x32x16 or 16x16x32 products -- and so its
-// rounding -- does not depend on how many clips share the launch.
+// convs, 64 -> 160) when ONE CLIP's map gives >= 128 blocks (every 112x112-clip layer1 map: 32x112x112
+// gives 392); everywhere else conv_patch_bf16 is as fast or faster (convbench, 30 clips,
+// profiles/r04_patch32_bf16.txt: layer1 0.686 vs 0.726 ms, layer2 288 channels at NB 3 0.325 vs 0.313,
+// layer3 576 at NB 3 0.152 vs 0.156, layer4 1152 at NB 2 0.114 vs 0.088). 0: not taken. force_nb > 0
+// (convbench, CLASFV_PATCH_NT = -NB) takes any NB that divides.
+// The rule counts blocks per clip, never the batch's, so whether a clip's layer1 runs 32x32x16 or
+// 16x16x32 products -- and so its rounding -- does not depend on how many clips share the launch. The
+// price is paid on small batches, where the r04 measurement found conv_patch_bf16 as fast or faster: a
+// deliberate determinism-over-speed trade (its cost at N = 1 and 4: profiles/r06*_patch32_small_batch.txt).
 int patch32_pick_nb(const ConvParams& p, int force_nb) {
   if (p.Cout % 32) return 0;
   const int n32 = p.Cout / 32;

@@ -612,15 +612,14 @@ void decoder_x3_weights(const float* w2, const float* wh, uint16_t* out) {
               3 * 4096 + (((size_t)kb * 16 + l) * 4 + q) * 8 + e, 1024);
 }
 
-// 16-row tiles (variant decoder_rows16, the fp32 engines' MODE 4 only): half the blocks and 0.8x the
-// staged halo per voxel, bit-identical; convbench 1.293 -> 1.256 ms per 30 clips on cold taps
-// (profiles/r05n_decoder_16row_tiles.txt), but 1.275-1.280 -> 1.289-1.294 in the forward, whose taps
-// were just written (profiles/r05p_decoder_rows_forward_ab.txt): 8 rows stay the product. (MODE 1 at
-// 16 rows: 1.176 -> 1.281 ms, a 512-thread block at 5 waves per SIMD leaves 4 resident.)
+// 8-row tiles. 16-row tiles (convbench ko + 16 only) are bit-identical; convbench 1.293 -> 1.256 ms per
+// 30 clips on cold taps (profiles/r05n_decoder_16row_tiles.txt), but 1.275-1.280 -> 1.289-1.294 in the
+// forward, whose taps were just written (profiles/r05p_decoder_rows_forward_ab.txt). (MODE 1 at 16 rows:
+// 1.176 -> 1.281 ms, a 512-thread block at 5 waves per SIMD leaves 4 resident.)
 hipError_t launch_decoder(const DecParams& p, hipStream_t s) {
   if ((p.x3 || p.bf16) && !p.w2x3) return hipErrorInvalidValue;  // the split-bf16 heads' Wh pieces
   const int mode = p.bf16 ? 1 : p.x3 ? 4 : 0;
-  return launch_dec(p, s, mode, mode == 4 && p.rows16 && p.H % 16 == 0 ? 16 : 8);
+  return launch_dec(p, s, mode, 8);
 }
 
 #ifdef CLASFV_KNOCKOUTS

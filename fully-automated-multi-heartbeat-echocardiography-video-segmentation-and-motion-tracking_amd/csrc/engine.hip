@@ -124,17 +124,22 @@ int env_variants() {
   if (on("CLASFV_NO_PATCH32")) f |= CLASFV_VARIANT_NO_PATCH32;
   if (on("CLASFV_NO_PROJ_X3")) f |= CLASFV_VARIANT_NO_PROJ_X3;
   if (on("CLASFV_NO_WINO4R")) f |= CLASFV_VARIANT_NO_WINO4R;
-  if (on("CLASFV_DECODER_ROWS16")) f |= CLASFV_VARIANT_DECODER_ROWS16;
   if (on("CLASFV_NO_DMA_BUF")) f |= CLASFV_VARIANT_NO_DMA_BUF;
   if (on("CLASFV_W4R_CACHED_STORES")) f |= CLASFV_VARIANT_W4R_CACHED_STORES;
-  if (on("CLASFV_WINOT_NT_STORES")) f |= CLASFV_VARIANT_WINOT_NT_STORES;
-  if (on("CLASFV_DMA_NT_STORES")) f |= CLASFV_VARIANT_DMA_NT_STORES;
   if (on("CLASFV_PATCH32_CACHED_STORES")) f |= CLASFV_VARIANT_PATCH32_CACHED_STORES;
-  if (on("CLASFV_PATCH_NT_STORES")) f |= CLASFV_VARIANT_PATCH_NT_STORES;
   if (on("CLASFV_NO_DMA_W")) f |= CLASFV_VARIANT_NO_DMA_W;
-  if (on("CLASFV_DMA_X3_WR")) f |= CLASFV_VARIANT_DMA_X3_WR;
   return f;
 }
+
+// every CLASFV_VARIANT_* bit of include/clasfv.h (the retired bits are rejected)
+constexpr int kVariantMask = CLASFV_VARIANT_NO_WINOGRAD | CLASFV_VARIANT_NO_WINO_PATCH | CLASFV_VARIANT_WINOT_REFERENCE |
+                             CLASFV_VARIANT_NO_C8 | CLASFV_VARIANT_NO_STEM_BF16 | CLASFV_VARIANT_NO_PATCH_BF16 |
+                             CLASFV_VARIANT_NO_DECODER_BF16 | CLASFV_VARIANT_WINOT_NO_TS1 | CLASFV_VARIANT_NO_SPLIT_K |
+                             CLASFV_VARIANT_NO_WINO4 | CLASFV_VARIANT_NO_DECODER_X3 | CLASFV_VARIANT_NO_DMA_X3 |
+                             CLASFV_VARIANT_NO_STEM_X3 | CLASFV_VARIANT_NO_WINO4W | CLASFV_VARIANT_NO_PATCH32 |
+                             CLASFV_VARIANT_NO_PROJ_X3 | CLASFV_VARIANT_NO_WINO4R | CLASFV_VARIANT_NO_DMA_BUF |
+                             CLASFV_VARIANT_W4R_CACHED_STORES | CLASFV_VARIANT_PATCH32_CACHED_STORES |
+                             CLASFV_VARIANT_NO_DMA_W;
 
 int env_int(const char* name) {
   const char* e = getenv(name);
@@ -171,7 +176,7 @@ int midplanes(int i, int o) { return (i * o * 27) / (i * 9 + 3 * o); }
 // Engine-wide kernel switches: CLASFV_VARIANT_* flags and the implicit-GEMM / patch-kernel tile
 // overrides (0: automatic).
 struct Tuning {
-  int vflags = 0, conv_nt = 0, conv_mt = 0, patch_nt = 0;
+  int vflags = 0, conv_nt = 0, patch_nt = 0;
 };
 
 }  // namespace
@@ -539,7 +544,6 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
     int mt = 2, bn = c.cout_p;  // stem: one N tile (48 fp32 / 64 bf16 channels)
     if (!c.stem) {
       conv_pick_tile(p.M, c.cout_p, tu.conv_nt, &mt, &bn);
-      if (tu.conv_mt == 4 && p.in_bf16) mt = 4;  // tuning override
       // split-K on the smallest maps (per-clip shape rule), partial sums in the caller's scratch
       const int S = dma_split_for(p, mt);
       if (S > 1 && scratch && (size_t)S * p.M * p.Cout * sizeof(float) <= scratch_bytes) {
@@ -644,7 +648,6 @@ int clasfv_create(int device, clasfv_t* out) {
   e->device = device;
   e->tune.vflags = env_variants();
   e->tune.conv_nt = env_int("CLASFV_CONV_NT");
-  e->tune.conv_mt = env_int("CLASFV_CONV_MT");
   e->tune.patch_nt = env_int("CLASFV_PATCH_NT");
   build_plan(e);
   *out = e;
@@ -902,7 +905,7 @@ int clasfv_get_compute_dtype(clasfv_t h) { return h ? h->dtype : CLASFV_EINVAL; 
 
 int clasfv_set_kernel_variants(clasfv_t h, int flags) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
-  if (flags & ~0x3FFFFFF) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
+  if (flags & ~kVariantMask) return fail(CLASFV_EINVAL, "unknown kernel-variant bit");
   if ((flags ^ h->tune.vflags) & CLASFV_VARIANT_NO_WINOGRAD) h->ready = false;  // weight images change
   h->tune.vflags = flags;
   return CLASFV_OK;
@@ -1071,7 +1074,6 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   d.bf16 = h->dtype == CLASFV_DTYPE_BF16 && !(h->tune.vflags & CLASFV_VARIANT_NO_DECODER_BF16);
   d.w2x3 = h->w2x3;
   d.x3 = h->dtype != CLASFV_DTYPE_BF16 && !(h->tune.vflags & CLASFV_VARIANT_NO_DECODER_X3);
-  d.rows16 = (h->tune.vflags & CLASFV_VARIANT_DECODER_ROWS16) != 0;
   HIP_TRY(launch_decoder(d, s));
   // comb_2 (64x64) and the heads (6 useful of the 16 rows of their MFMA tile) per output voxel, in the
   // products of the pipe they run on: fp32 engines six split-bf16 products each (bf16 pipe), bf16

@@ -19,9 +19,11 @@ struct W4Geo {
   int n_cob;    // output-channel blocks (cob_w channels each) per tile group
   int gpr;      // groups per flattened tile row (TW / TC)
   FastDiv fd_cob, fd_gpr, fd_th, fd_tc, fd_rp, fd_ss;
-  // conv_wino4r start stagger: first-round block b waits ((b / 8) % stagger_groups) * stagger ticks of
-  // the 100-MHz real-time clock before its first DMA (0: none)
+#ifdef CLASFV_KNOCKOUTS
+  // conv_wino4r start stagger (convbench probe, profiles/r05ag_*: ±0): first-round block b waits
+  // ((b / 8) % stagger_groups) * stagger ticks of the 100-MHz real-time clock before its first DMA
   int stagger, stagger_groups;
+#endif
 };
 
 namespace {
@@ -98,8 +100,10 @@ __device__ inline void bt_cols(const f32x2 (&t)[6], f32x2 (&v)[3]) {
 // At 56x56 maps (TW = 14) that is 8 rows x 2 tiles instead of 1 x 14: 16 of 16 MFMA rows carry tiles
 // instead of 14, for 20 % more raw-patch bytes per tile.
 inline bool wino4_geometry(const ConvParams& p, W4Geo* g, int* n_blocks, int cob_w = 48, int fill16 = 0) {
+#ifdef CLASFV_KNOCKOUTS
   g->stagger = 0;
   g->stagger_groups = 1;
+#endif
   if (p.Cout % cob_w || p.Cin % 8) return false;
   const int TH = (p.Ho + 3) / 4, TW = (p.Wo + 3) / 4;
   const long rows = (long)p.N * p.To * TH;  // flattened tile rows

@@ -485,7 +485,8 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
   unsigned long long st_[4] = {0, 0, 0, 0};
   if constexpr ((KO & 512) != 0) st_[0] = __builtin_amdgcn_s_memrealtime();
 #endif
-  // start stagger (W4Geo::stagger): blocks of equal work started together stay in lockstep, and all
+#ifdef CLASFV_KNOCKOUTS
+  // (convbench only) start stagger (W4Geo::stagger): blocks of equal work started together stay in lockstep, and all
   // 256 CUs then run their epilogues -- the output stores -- at once, reading nothing meanwhile
   // (profiles/r05ag_wino4r_epilogue_concurrency.txt); first-round blocks 8 j .. 8 j + 7 (one per XCD)
   // start (j % groups) stagger ticks apart, so the epilogues of different CUs fall in different phases
@@ -496,6 +497,7 @@ __global__ __launch_bounds__(W4R_THREADS) __attribute__((amdgpu_waves_per_eu(3, 
       while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
     }
   }
+#endif
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(p.x), (short)0, (int)((size_t)p.N * p.Ti * p.Hi * p.Wi * p.Cin * 4), 0x00020000);
   const int tid = threadIdx.x, lane = tid & 63;

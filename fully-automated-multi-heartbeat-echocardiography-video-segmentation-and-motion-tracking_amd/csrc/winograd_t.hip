@@ -532,10 +532,6 @@ hipError_t winot5_launch(const ConvParams& p, hipStream_t s) {
     if (e != hipSuccess) return e;
     return launch_split_sum(p, s);
   }
-  if (p.vflags & CLASFV_VARIANT_WINOT_NT_STORES) {  // A/B: non-temporal output stores
-    if (p.res && p.relu) return winot5_launch_e<TS, NT, 3 + X + 32768>(p, s);
-    if (p.relu) return winot5_launch_e<TS, NT, 2 + X + 32768>(p, s);
-  }
   switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
     case 2: return winot5_launch_e<TS, NT, 2 + X>(p, s);  // TP1 / stem T: BN + ReLU
     case 3: return winot5_launch_e<TS, NT, 3 + X>(p, s);  // TP2: BN + residual + ReLU

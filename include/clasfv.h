@@ -59,7 +59,8 @@ enum { CLASFV_DTYPE_FP32 = 0, CLASFV_DTYPE_BF16 = 1 };
  * variant computes the same function -- NO_SPLIT_K the same sums in another fp32 summation order,
  * NO_WINO4 the same convolutions through F(2x2,3x3) instead of F(4x4,3x3) fp32 rounding).
  * Read once, at clasfv_create, from the environment variable named in the comment (set = on), or set
- * with clasfv_set_kernel_variants. */
+ * with clasfv_set_kernel_variants. Bits 131072, 1048576, 2097152, 8388608 and 33554432 are retired
+ * (round-5 A/B forms that measured slower; they live only in tools/convbench now) and rejected. */
 enum {
   CLASFV_VARIANT_NO_WINOGRAD = 1,      /* CLASFV_WINOGRAD=0: fp32 stride-1 convs on the direct implicit GEMM */
   CLASFV_VARIANT_NO_WINO_PATCH = 2,    /* CLASFV_NO_WINO_PATCH: conv_wino instead of conv_wino_q */
@@ -78,15 +79,10 @@ enum {
   CLASFV_VARIANT_NO_PATCH32 = 16384,   /* CLASFV_NO_PATCH32: bf16 1x3x3 convs on conv_patch_bf16 (16x16x32 tiles) instead of conv_patch32_bf16 (32x32x16) */
   CLASFV_VARIANT_NO_PROJ_X3 = 32768,   /* CLASFV_NO_PROJ_X3: the decoder's 128-deep tap projections on conv_dma_x3 instead of the persistent conv_proj_x3 */
   CLASFV_VARIANT_NO_WINO4R = 65536,    /* CLASFV_NO_WINO4R: wide-block 1x3x3 convs on conv_wino4w (4 quadrant waves, one per SIMD) instead of conv_wino4r (12 row waves, three per SIMD) */
-  CLASFV_VARIANT_DECODER_ROWS16 = 131072, /* CLASFV_DECODER_ROWS16: the fp32 engines' decoder on 16 x 16-voxel tiles instead of 8 x 16 (bit-identical; 1 % slower in the forward) */
   CLASFV_VARIANT_NO_DMA_BUF = 262144,  /* CLASFV_NO_DMA_BUF: conv_dma_x3's LDS-DMAs from 64-bit pointers instead of 32-bit buffer offsets */
   CLASFV_VARIANT_W4R_CACHED_STORES = 524288, /* CLASFV_W4R_CACHED_STORES: conv_wino4r's output stores cached instead of non-temporal */
-  CLASFV_VARIANT_WINOT_NT_STORES = 1048576, /* CLASFV_WINOT_NT_STORES: conv_winot5's output stores non-temporal (A/B) */
-  CLASFV_VARIANT_DMA_NT_STORES = 2097152,   /* CLASFV_DMA_NT_STORES: conv_dma_x3's output stores non-temporal (A/B) */
   CLASFV_VARIANT_PATCH32_CACHED_STORES = 4194304, /* CLASFV_PATCH32_CACHED_STORES: conv_patch32_bf16's output stores cached (the product's are non-temporal) */
-  CLASFV_VARIANT_PATCH_NT_STORES = 8388608, /* CLASFV_PATCH_NT_STORES: conv_patch_bf16's output stores non-temporal (A/B) */
-  CLASFV_VARIANT_NO_DMA_W = 16777216,       /* CLASFV_NO_DMA_W: the bf16 engines' direct convs on conv_dma (64-B LDS rows) instead of conv_dma_w (128-B rows) */
-  CLASFV_VARIANT_DMA_X3_WR = 33554432       /* CLASFV_DMA_X3_WR: conv_dma_x3 with 128-B A rows (A/B; slower) */
+  CLASFV_VARIANT_NO_DMA_W = 16777216        /* CLASFV_NO_DMA_W: the bf16 engines' direct convs on conv_dma (64-B LDS rows) instead of conv_dma_w (128-B rows) */
 };
 
 typedef struct clasfv_engine* clasfv_t;
