@@ -43,7 +43,8 @@ GFLOP_PER_CLIP_C3 = 1340.68      # 64x224x224 clip, BASELINE.md §2
 FP32_PEAK_TFLOPS = 157.3         # MI355X fp32 (vector = MFMA), MI355X_MICROARCH.md
 BF16_PEAK_TFLOPS = 2500.0        # MI355X bf16 MFMA dense
 NORTHSTAR = {"echo": os.path.join(REPO, "tests", "golden", "northstar_c1.npz"),
-             "random": os.path.join(REPO, "tests", "golden", "northstar_c1_random.npz")}
+             "random": os.path.join(REPO, "tests", "golden", "northstar_c1_random.npz"),
+             "deep": os.path.join(REPO, "tests", "golden", "northstar_c1_deep.npz")}
 BENCH_WEIGHTS = "echo"           # seeded weights whose masks follow the synthetic LV (weights.echo_state_dict)
 DICE_BAR = {"fp32": 1e-3, "bf16": 1e-2}  # north_star: Dice within 1e-3 (fp32), 1e-2 (bf16/fp16)
 
@@ -64,8 +65,9 @@ def parse(argv=None):
     ap.add_argument("--batch-size", type=int, default=32, help="clips per forward call")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--parity-random", type=int, default=1,
-                    help="also check the same workload with the random weight recipe against its CPU fixture "
-                         "(one untimed step; reported as 'parity_random_weights')")
+                    help="also check the same workload with the random and deep weight recipes against their CPU "
+                         "fixtures (one untimed step each; reported as 'parity_random_weights' / "
+                         "'parity_deep_weights', and in the bf16 object)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal, several ranks on one GPU)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"], help="encoder compute dtype of the headline run")
     ap.add_argument("--extra-bf16", type=int, default=1,
@@ -319,17 +321,18 @@ def northstar_parity(args, fused_video0, dtype, recipe=BENCH_WEIGHTS):
                          % (os.path.basename(path), args.fuse_method)}
 
 
-def random_recipe_parity(args, model, step, dtype):
-    """One untimed step of the same workload with the "random" weight recipe (every layer at full gain:
-    the echo recipe's LV decision runs through the stem, layer1 and the decoder only) against its CPU
-    fixture; the bench weights are restored afterwards."""
+def random_recipe_parity(args, model, step, dtype, recipe="random"):
+    """One untimed step of the same workload with another weight recipe against its CPU fixture; the
+    bench weights are restored afterwards. "random": every layer at full gain (the echo recipe's LV
+    decision runs through the stem, layer1 and the decoder only), degenerate EFs; "deep": the echo
+    segmentation routed through layer2-4 at full gain, physiological EFs."""
     import clasfv_amd.weights as W
-    if not os.path.exists(NORTHSTAR["random"]):
+    if not os.path.exists(NORTHSTAR[recipe]):
         return None
-    model.load_state_dict(W.recipe_state_dict("random", W.DEFAULT_SEED))
+    model.load_state_dict(W.recipe_state_dict(recipe, W.DEFAULT_SEED))
     try:
         out = step()
-        return northstar_parity(args, out[0], dtype, recipe="random") if 0 in out else None
+        return northstar_parity(args, out[0], dtype, recipe=recipe) if 0 in out else None
     finally:
         model.load_state_dict(W.recipe_state_dict(BENCH_WEIGHTS, W.DEFAULT_SEED))
 
@@ -585,6 +588,8 @@ def run_c1(args, model, world, rank, dev):
     lv_frac = float(np.mean([o.float().mean().item() for o in out.values()])) if out else 0.0
     parity = northstar_parity(args, out[0], args.dtype) if 0 in out else None
     parity_random = random_recipe_parity(args, model, step, args.dtype) if world == 1 and args.parity_random else None
+    parity_deep = (random_recipe_parity(args, model, step, args.dtype, "deep")
+                   if world == 1 and args.parity_random else None)
 
     bf16 = None
     if args.extra_bf16 and args.dtype == "fp32":
@@ -600,6 +605,8 @@ def run_c1(args, model, world, rank, dev):
                 "parity_vs_cpu": northstar_parity(args, out16[0], "bf16") if 0 in out16 else None,
                 "parity_vs_cpu_random_weights": (random_recipe_parity(args, model, step, "bf16")
                                                  if world == 1 and args.parity_random else None),
+                "parity_vs_cpu_deep_weights": (random_recipe_parity(args, model, step, "bf16", "deep")
+                                               if world == 1 and args.parity_random else None),
                 "roofline": kernel_roofline(k16, BF16_PEAK_TFLOPS, "bf16"),
                 "kernels": kernel_table(k16, "bf16"),
                 "note": "BASELINE config[4]: bf16 activations/weights, fp32 accumulate, fp32 decoder head; "
@@ -674,6 +681,7 @@ def run_c1(args, model, world, rank, dev):
         "ef_delta_vs_cpu": parity and parity["ef_delta_max_per_systole"],
         "parity": parity,
         "parity_random_weights": parity_random,
+        "parity_deep_weights": parity_deep,
         "bf16": bf16,
         "config3": c3,
         "c2_ragged": c2r,

@@ -178,7 +178,90 @@ def echo_state_dict(seed=DEFAULT_SEED, p=None):
     return sd
 
 
-RECIPES = {"random": synthetic_state_dict, "echo": echo_state_dict}
+# "deep" recipe constants (see deep_state_dict)
+DEEP = {
+    "g_deep": 1.0,                     # branch gain of the designed channels in layer2-4 (full gain)
+    "alpha": (0.7, 0.2, 0.07, 0.03),   # share of the layer1..layer4 taps in the band's intensity
+    "floor": 0.172,                    # layer1 intensity below which a pixel is never LV
+    # echo constants changed for this recipe: the blurred deep taps raise the intensity at the centre
+    # of the narrow end-systolic LV, so the band reaches higher (and the dark-and-edge veto with it)
+    "echo": {"band": (0.168, 0.25, 0.34), "dark": 0.35},
+}
+
+
+def deep_state_dict(seed=DEFAULT_SEED, p=None):
+    """The "echo" segmentation routed through the WHOLE encoder at full gain (round 6).
+
+    In the echo recipe the LV decision reads only the layer1 tap, so layer2-4 reach the logits at
+    ~1e-4 and a bf16 engine's rounding there never moves a mask. Here the 6 designed channels
+    (intensity, 4 rectified gradients, intensity end correction) also run through every BasicBlock
+    of layer2-4 at full gain: the residual carries them (the strided 1x1x1 downsample as an identity
+    per channel) and the branch adds a 3x3 box smoothing of each (sp1 / sp2 box, tp1 / tp2 centre
+    tap, BN gamma g_deep) -- real 9-tap accumulations in bf16 weights and activations. comb_1's band
+    rows read the intensity as a mix of all four taps (alpha: layer1 .. layer4, each normalised by its
+    tap's gain), so roughly 60 % of the band input has passed through layer2-4 and been trilinearly
+    upsampled from 28^2, 14^2 and 7^2 maps. The edge veto keeps reading layer1's gradients. Every
+    other weight is the echo recipe's (random full-gain channels everywhere else)."""
+    q = dict(DEEP, **(p or {}))
+    pe = dict(q["echo"], **(p or {}))
+    sd = echo_state_dict(seed, pe)
+    e = dict(ECHO, **pe)
+    R = "r2plus1d_model."
+    nd = 6
+    g = q["g_deep"]
+    box = np.full((3, 3), 1.0 / 9.0, np.float32)
+    for li in (2, 3, 4):
+        for b in range(2):
+            pre = f"{R}layer{li}.{b}."
+            for conv, bn, kind in (("conv1.0.0", "conv1.0.1", "box"), ("conv1.0.3", "conv1.1", "tap"),
+                                   ("conv2.0.0", "conv2.0.1", "box"), ("conv2.0.3", "conv2.1", "tap")):
+                w = sd[pre + conv + ".weight"]
+                w[:nd] = 0.0
+                for k in range(nd):
+                    if kind == "box":
+                        w[k, k, 0] = box
+                    else:
+                        w[k, k, 1] = 1.0
+                # the branch gain once per half (conv1's BN after the temporal conv, conv2's likewise)
+                _identity_bn(sd, pre + bn, range(nd), gamma=g if kind == "tap" and conv == "conv2.0.3" else 1.0)
+            if b == 0:
+                w = sd[pre + "downsample.0.weight"]
+                w[:nd] = 0.0
+                for k in range(nd):
+                    w[k, k, 0, 0, 0] = 1.0
+                _identity_bn(sd, pre + "downsample.1", range(nd))
+    # per-tap gain of the designed intensity: layer1 (1 + g1)^2 S0, then (1 + g_deep) per block
+    unit1 = (1.0 + e["g"]) ** 2 * e["S0"]
+    units = [unit1 * (1.0 + g) ** (2 * i) for i in range(4)]
+    col0 = (64, 128, 256, 512)  # concat column of each tap's channel 0 (layer1 .. layer4)
+    w1 = sd["comb_1_layer.weight"].reshape(64, 1024)
+    b1 = sd["comb_1_layer.bias"]
+    lo, mid, hi = e["band"]
+    for r, t in enumerate((lo, mid, hi)):
+        w1[r, [64, 69]] = 0.0
+        for a, u, c in zip(q["alpha"], units, col0):
+            w1[r, [c, c + 5]] = a * e["c"] / u
+        b1[r] = -e["c"] * t
+    # "very dark" veto: the blurred deep taps put the band on the dark side of the sector's border,
+    # beyond the reach of layer1's edge indicator; r7 - r8 = clamp(k (floor - L1), 0, 1) on layer1's
+    # intensity (outside the sector ~0.12, blood pool ~0.19-0.21) drives comb_2 row 2 and the seg head
+    k = e["k"]
+    w1[7:9] *= e["noise"]
+    for r, off in ((7, 0.0), (8, -1.0)):
+        w1[r, [64, 69]] = -k / unit1
+        b1[r] = k * q["floor"] + off
+    _identity_bn(sd, "comb_batch_norm_1", [7, 8])
+    w2 = sd["comb_2_layer.weight"].reshape(64, 64)
+    b2 = sd["comb_2_layer.bias"]
+    w2[2] *= e["noise"]
+    w2[2, 7:9] = (1.0, -1.0)
+    b2[2] = 0.0
+    _identity_bn(sd, "comb_batch_norm_2", [2])
+    sd["segmentation_head.weight"].reshape(2, 64)[1, 2] = -e["A_edge"]
+    return sd
+
+
+RECIPES = {"random": synthetic_state_dict, "echo": echo_state_dict, "deep": deep_state_dict}
 
 
 def recipe_state_dict(recipe="random", seed=DEFAULT_SEED):

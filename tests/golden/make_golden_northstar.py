@@ -8,7 +8,11 @@ workload -- with one of two seeded weight recipes:
           the synthetic LV, so the EFs are physiological (~77 %); the LV decision runs through the
           stem, layer1 and the decoder (layer2-4 reach the logits at ~1e-2 of the margin);
   random  (northstar_c1_random.npz) weights.synthetic_state_dict(DEFAULT_SEED): every layer at full
-          gain, so every conv of the encoder moves the fused masks (EFs degenerate).
+          gain, so every conv of the encoder moves the fused masks (EFs degenerate);
+  deep    (northstar_c1_deep.npz, round 6) weights.deep_state_dict(DEFAULT_SEED): the echo
+          segmentation routed through layer2-4 at full gain (about 60 % of the band's intensity input
+          passes through them), so bf16 rounding anywhere in the encoder reaches masks with
+          physiological EFs.
 Everything is
 computed by the oracle (tests-only infrastructure): the torch-CPU restatement of the reference model
 (oracle/r2plus1d_ref.py, pinned to the reference module by tests/golden/model_forward.npz) and the
@@ -38,7 +42,7 @@ from oracle import fuse_ref, r2plus1d_ref  # noqa: E402
 
 T, F, STEP, SEED = 200, 5, 1, 0
 RECIPE = sys.argv[1] if len(sys.argv) > 1 else "echo"
-OUT = {"echo": "northstar_c1.npz", "random": "northstar_c1_random.npz"}[RECIPE]
+OUT = {"echo": "northstar_c1.npz", "random": "northstar_c1_random.npz", "deep": "northstar_c1_deep.npz"}[RECIPE]
 METHODS = ("majority", "simple", "staple")
 
 

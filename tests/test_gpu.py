@@ -45,6 +45,13 @@ def echo_model():
     return R2plus1D_18_MotionNet(pretrained=False, weights="echo")
 
 
+@pytest.fixture(scope="module")
+def deep_model():
+    """The "deep" recipe: the echo segmentation routed through layer2-4 at full gain."""
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    return R2plus1D_18_MotionNet(pretrained=False, weights="deep")
+
+
 def test_native_library_is_loaded(model):
     import clasfv_amd._lib as L
     with open("/proc/self/maps") as f:
@@ -825,7 +832,7 @@ def test_c8_blocked_mid_bitexact(model, shape):
 
 # ---- north_star bar on BASELINE config[1] (round 2) -----------------------------------------------
 
-NORTHSTAR_FIXTURES = {"echo": "northstar_c1.npz", "random": "northstar_c1_random.npz"}
+NORTHSTAR_FIXTURES = {"echo": "northstar_c1.npz", "random": "northstar_c1_random.npz", "deep": "northstar_c1_deep.npz"}
 
 
 def _northstar(recipe="echo"):
@@ -839,10 +846,13 @@ def _northstar(recipe="echo"):
 def _recipe_model(request, recipe):
     # echo: the bench's weights (masks follow the LV, physiological EFs; layer2-4 reach the LV margin
     # at ~1e-2 only). random: every layer at full gain, so every conv of the encoder moves the masks.
+    # deep (round 6): the echo segmentation routed through layer2-4 at full gain.
+    if recipe == "deep":
+        return request.getfixturevalue("deep_model")
     return request.getfixturevalue("echo_model" if recipe == "echo" else "model")
 
 
-@pytest.mark.parametrize("recipe", ["echo", "random"])
+@pytest.mark.parametrize("recipe", ["echo", "random", "deep"])
 def test_northstar_config1_pass_labels_vs_cpu(request, recipe):
     """Config[1] (200 frames, 5 shifted passes, 30 clips) through the real HIP model: every pass's
     label video (clips built on the GPU, batched forward, softmax -> resample -> argmax) against the
@@ -866,7 +876,7 @@ def test_northstar_config1_pass_labels_vs_cpu(request, recipe):
         assert (got != ref).mean() <= 1e-4, j
 
 
-@pytest.mark.parametrize("recipe", ["echo", "random"])
+@pytest.mark.parametrize("recipe", ["echo", "random", "deep"])
 @pytest.mark.parametrize("method", ["majority", "simple", "staple"])
 def test_northstar_config1_fused_masks_and_ef_vs_cpu(request, recipe, method):
     """north_star bar (BASELINE.json): fused masks Dice delta <= 1e-3 and EF within 1e-3 of the CPU
@@ -891,8 +901,8 @@ def test_northstar_config1_fused_masks_and_ef_vs_cpu(request, recipe, method):
     assert np.array(pairs, np.int64).reshape(-1, 2).tolist() == g[f"pairs_{method}"].tolist()
     # random recipe: EFs ~100 % (ES volume ~0), where a one-pixel change moves the EF by ~1e-3
     np.testing.assert_allclose(np.array(efs, np.float64), g[f"ef_{method}"], rtol=0,
-                               atol=1e-3 if recipe == "echo" else 1e-2, equal_nan=True)
-    if recipe == "echo":  # physiological: the masks follow the LV
+                               atol=1e-2 if recipe == "random" else 1e-3, equal_nan=True)
+    if recipe != "random":  # physiological: the masks follow the LV
         assert np.all((30 < g[f"ef_{method}"]) & (g[f"ef_{method}"] < 80))
 
 
@@ -1014,7 +1024,7 @@ def test_video_stream_matches_per_video_pipeline(model):
 
 # ---- round 3: config[4] on the north_star video, CLI vs the CPU path, non-strict plumbing -------
 
-@pytest.mark.parametrize("recipe", ["echo", "random"])
+@pytest.mark.parametrize("recipe", ["echo", "random", "deep"])
 def test_northstar_config4_bf16_fused_masks_vs_cpu(recipe):
     """BASELINE config[4] bar on the config[1] video: the bf16 engine's fused masks (SIMPLE, 5 passes)
     against the CPU reference path's fp32 masks: Dice delta <= 1e-2 and EF close. Both weight recipes:
@@ -1037,7 +1047,11 @@ def test_northstar_config4_bf16_fused_masks_vs_cpu(recipe):
     print(f"config[4] {recipe}: Dice delta {d:.3e}, EFs {np.round(efs, 3).tolist()} vs "
           f"{np.round(g['ef_simple'], 3).tolist()}, pairs {np.array(pairs).reshape(-1, 2).tolist()}")
     assert d <= 1e-2, d
-    if recipe == "echo":
+    if recipe in ("echo", "deep"):
+        # deep (round 6): the band's intensity is 30 % layer2-4 taps at full gain (a 1 % change of those
+        # taps flips ~18 mask pixels per clip on the CPU path, none with the echo weights), so here bf16
+        # rounding anywhere in the encoder reaches masks with physiological EFs (~78.5 %): same ED/ES
+        # pairs, every EF within 1 point
         assert np.array(pairs, np.int64).reshape(-1, 2).tolist() == g["pairs_simple"].tolist()
         np.testing.assert_allclose(np.array(efs, np.float64), g["ef_simple"], rtol=0, atol=1.0)
     else:

@@ -210,3 +210,34 @@ def test_northstar_fixture_is_physiological():
         efs = g[f"ef_{m}"]
         assert len(efs) == 4 and np.all((30 < efs) & (efs < 80)), efs
         assert g[f"pairs_{m}"].tolist() == [[0, 25], [50, 75], [100, 125], [150, 175]]
+
+
+def test_deep_fixture_is_physiological_and_depends_on_layer2_4():
+    """tests/golden/northstar_c1_deep.npz (round 6: the "deep" weights route the echo segmentation
+    through layer2-4 at full gain): physiological EFs on the video's cycles, and the oracle's masks
+    move when only the layer2-4 taps move (x 0.99: the size of accumulated bf16 rounding), which they
+    never do with the echo weights -- so config[4]'s EF leg on this fixture sees bf16 arithmetic in
+    every layer of the encoder."""
+    import torch
+    import clasfv_amd.synthetic as S
+    import clasfv_amd.weights as W
+    g = golden("northstar_c1_deep.npz")
+    assert str(g["weights_recipe"]) == "deep"
+    for m in ("majority", "simple", "staple"):
+        efs = g[f"ef_{m}"]
+        assert len(efs) == 4 and np.all((60 < efs) & (efs < 85)), efs
+        assert np.all(np.abs(g[f"pairs_{m}"] - [[0, 25], [50, 75], [100, 125], [150, 175]]) <= 1)
+    shp = tuple(g["fused_simple_shape"])
+    fused = np.unpackbits(g["fused_simple"])[: int(np.prod(shp))].reshape(shp)
+    assert fused[25::50].sum((1, 2)).min() > 200  # non-empty end-systolic masks
+    v = fuse_ref.zeroone_normalizer(S.echo_video(32, seed=0))
+    x = torch.from_numpy(np.ascontiguousarray(v[None]))
+    flips = {}
+    for rec in ("echo", "deep"):
+        sd = W.recipe_state_dict(rec)
+        with torch.no_grad():
+            taps = r2plus1d_ref.backbone(sd, x)
+            s0, _ = r2plus1d_ref.head(sd, taps)
+            s1, _ = r2plus1d_ref.head(sd, taps[:2] + [t * 0.99 for t in taps[2:]])
+        flips[rec] = int(((s0[0, 1] > s0[0, 0]) != (s1[0, 1] > s1[0, 0])).sum())
+    assert flips["echo"] == 0 and flips["deep"] > 0, flips
