@@ -821,6 +821,376 @@ hipError_t launch_patch32_bf16_epi(const ConvParams& p, hipStream_t s, int epi) 
 }
 #endif
 
+// ---------------------------------------------------------------------------------------------
+// (convbench only, round 6: measured no faster than conv_dma_w -- layer2 0.390-0.396 vs 0.399 ms,
+// layer3 0.143-0.145 vs 0.145, layer4 0.075-0.081 vs 0.067; profiles/r06b_patch_s2_bf16.txt)
+#ifdef CLASFV_KNOCKOUTS
+// conv_patch_s2_bf16 (round 6): the strided spatial convs (1x3x3, stride (1,2,2), pad (0,1,1)) of the
+// Conv2Plus1D first halves of layer2-4 (torchvision Conv2Plus1D via src/model/R2plus1D_18_MotionNet.py:33-37)
+// in the bf16 engines. conv_dma_w gathers one 128-B tap row per output voxel and tap (9 x 64 rows per
+// 8x8 output tile and 32 channels); here a block DMAs the tile's 17x17-pixel input patch once per
+// 32-channel chunk (289 rows) and every tap reads its A fragments from it.
+//  * polyphase patch: the patch is stored as its 4 (row, column) parity sub-grids of 9 x 9 slots
+//    (phase-1 grids use 8 x 8 of them). Tap (kh, kw) of output pixel (oy, ox) reads input (2 oy + kh,
+//    2 ox + kw) = sub-grid (kh & 1, kw & 1), slot (oy + kh / 2, ox + kw / 2): every tap reads runs of
+//    consecutive slots, as a stride-1 conv does, and the 16-B slot q of slot (row sr, col sc) is stored
+//    at q ^ 2 (sr & 1) -- conflict-free for every tap's ds_read_b128 lane groups (the two output rows
+//    of a 16-voxel m tile sit on sub-grid rows of opposite parity);
+//  * sub-grid-major LDS image [4 sub-grids][FR frames][81 slots] (each sub-grid image padded to whole
+//    1-KiB DMA pieces), ONE buffer: the taps run sub-grid by sub-grid -- (0,0) (0,2) (2,0) (2,2), then
+//    (0,1) (2,1), (1,0) (1,2), (1,1) -- and each sub-grid of the next chunk is DMA'd as soon as the
+//    step barrier shows every wave past its last tap (5-8 steps before it is read), so the patch is
+//    single-buffered and two blocks fit a CU;
+//  * the rest is conv_patch_bf16: 16x16x32 MFMAs with D^T = W . A^T, wave w owns m tiles MT w ..
+//    MT w + MT - 1 (FR frames x 64 voxels per block), B ring of S stages (weights w[n][tap Cin + c],
+//    conv_dma's image), LDS-staged epilogue.
+// K order: chunk-major, then the tap order above: not conv_dma_w's (tap-major) fp32 summation order,
+// so outputs match it within bf16 rounding, not bit for bit.
+namespace {
+
+constexpr int S2_ORDER[9] = {0, 2, 6, 8, 1, 7, 3, 5, 4};  // tap (kh * 3 + kw) of each step of a chunk
+
+template <int FR>
+struct S2Geo {
+  static constexpr int PITCH = 9, SUB = 81;                    // sub-grid slots: 9 rows x 9 columns
+  static constexpr int SUBP = (FR * SUB + 15) / 16;            // 1-KiB pieces per sub-grid image
+  static constexpr int PW = (SUBP + 3) / 4;                    // DMAs per wave per sub-grid image
+  static constexpr int SUBB = SUBP * 1024;                     // bytes per sub-grid image
+  static constexpr int BYTES = 4 * SUBB;
+};
+
+template <int NT, int FR, int S, int OCC, int EF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void conv_patch_s2_bf16(
+    ConvParams p, int n_tiles, int ptw, int npt, int t_tiles) {
+  using G = S2Geo<FR>;
+  constexpr int MT = FR, PW = G::PW, BW = (NT + 3) / 4;
+  constexpr int B_STAGE = NT * 1024, B0 = G::BYTES, SINK = B0 + S * B_STAGE;
+  constexpr int LDS = SINK + 1024;
+  static_assert(OCC * LDS <= 160 * 1024, "LDS budget");
+  static_assert(S == 2 || S == 3, "wait counts below");
+  __shared__ __align__(16) char smem[LDS];
+
+  const __bf16* x = reinterpret_cast<const __bf16*>(p.x);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, l16 = lane & 15;
+  int tile = xcd_swizzle_p(blockIdx.x, gridDim.x);
+  const int n0 = (tile % n_tiles) * 16 * NT;
+  tile /= n_tiles;
+  const int pt = tile % npt;
+  tile /= npt;
+  const int t0 = (tile % t_tiles) * FR;
+  const int clip = tile / t_tiles;
+  const int h0 = (pt / ptw) * 8, w0 = (pt % ptw) * 8;  // output tile origin
+  const int Cin = p.Cin;
+
+  // patch DMA of one sub-grid image: piece j = wid + 4 i writes slots 16 j .. 16 j + 15 of it, lane ->
+  // slot 16 j + lane / 4 = frame f, row sr, column sc; pieces past the image land in the sink, slots
+  // past the patch (the phase-1 grids' ninth row / column) read the zero block
+  int pv[4][PW];
+  unsigned psl[4][PW];
+#pragma unroll
+  for (int sg = 0; sg < 4; ++sg)
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int slot = (wid + 4 * i) * 16 + (lane >> 2);
+      const int f = slot / G::SUB, r = slot - f * G::SUB, sr = r / G::PITCH, sc = r - sr * G::PITCH;
+      const int pr = 2 * sr + (sg >> 1), pc = 2 * sc + (sg & 1);
+      psl[sg][i] = (unsigned)(((lane & 3) ^ (2 * (sr & 1))) * 16);
+      pv[sg][i] = -1;
+      const int ti = t0 + f, hi = 2 * h0 - 1 + pr, wi = 2 * w0 - 1 + pc;
+      if (f < FR && pr <= 16 && pc <= 16 && ti < p.Ti && (unsigned)hi < (unsigned)p.Hi && (unsigned)wi < (unsigned)p.Wi)
+        pv[sg][i] = ((clip * p.Ti + ti) * p.Hi + hi) * p.Wi + wi;
+    }
+  auto issue_sub = [&](int c, int sg) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int j = wid + 4 * i;
+      const void* src = pv[sg][i] >= 0
+                            ? (const void*)(reinterpret_cast<const char*>(x + (size_t)pv[sg][i] * Cin + 32 * c) + psl[sg][i])
+                            : p.zero;
+      dma16(src, smem + (j < G::SUBP ? sg * G::SUBB + j * 1024 : SINK));
+    }
+  };
+  const char* wb = reinterpret_cast<const char*>(p.w) + (size_t)n0 * p.Kp * 2;
+  unsigned boff[BW];
+  {
+    const int drow = lane >> 2, dq = (lane & 3) ^ gsw((drow >> 2) & 3);
+#pragma unroll
+    for (int i = 0; i < BW; ++i) {
+      const int j = wid + 4 * i;
+      boff[i] = (unsigned)(((j < NT ? j : 0) * 16 + drow) * p.Kp + 8 * dq) * 2u;
+    }
+  }
+  const int nc = Cin / 32;
+  auto issue_b = [&](int c, int tap, int slot) __attribute__((always_inline)) {
+    const char* base = wb + (size_t)(tap * Cin + 32 * (c < nc ? c : 0)) * 2;
+#pragma unroll
+    for (int i = 0; i < BW; ++i) {
+      const int j = wid + 4 * i;
+      dma16(base, boff[i], smem + (j < NT ? B0 + slot * B_STAGE + j * 1024 : SINK));
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // A fragment i of this lane: block voxel m = 16 (MT wid + i) + l16 = frame f, pixel (oy, ox) of the
+  // 8x8 tile; LDS byte address of its 16-B slot q at every tap
+  int aaddr[9][MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int m = 16 * (MT * wid + i) + l16, f = m >> 6, px = m & 63, oy = px >> 3, ox = px & 7;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int kh = tap / 3, kw = tap % 3, sg = ((kh & 1) << 1) | (kw & 1);
+      const int sr = oy + (kh >> 1), sc = ox + (kw >> 1);
+      const int slot = f * G::SUB + sr * G::PITCH + sc;
+      aaddr[tap][i] = sg * G::SUBB + slot * 64 + ((q ^ (2 * (sr & 1))) << 4);
+    }
+  }
+  const int b_rd = B0 + l16 * 64 + (q ^ gsw(l16 >> 2)) * 16;
+
+  // prologue: sub-grids (0,0), (0,1), (1,0) of chunk 0 (sub-grid (1,1) goes out at chunk 0's step 0),
+  // then the first S - 1 weight steps
+  issue_sub(0, 0);
+  issue_sub(0, 1);
+  issue_sub(0, 2);
+#pragma unroll
+  for (int k = 0; k < S - 1; ++k) issue_b(k / 9, S2_ORDER[k % 9], k);
+  int slot = 0;
+
+  for (int c = 0; c < nc; ++c) {
+    const bool more = c + 1 < nc;
+    for_taps(std::make_integer_sequence<int, 9>{}, [&](auto tc) __attribute__((always_inline)) {
+      constexpr int T = decltype(tc)::value;
+      // Each step issues B(step + S - 1), then at most one sub-grid image: step 0 sub-grid (1,1) of
+      // this chunk, steps 4 / 6 / 8 sub-grids (0,0) / (0,1) / (1,0) of the next. A step needs B(step)
+      // and, at steps 0 / 4 / 6 / 8, a sub-grid image issued 5-8 steps earlier -- older than B(step)
+      // -- so it may leave in flight what was issued after B(step): the images of the last S - 1
+      // steps and (S = 3) one weight step.
+      constexpr int TP1 = (T + 8) % 9, TP2 = (T + 7) % 9;  // the previous two steps' tap positions
+      auto img = [&](int tp, bool same_chunk_more, bool prev_chunk) -> int {
+        // sub-grid DMAs issued at step position tp (of this chunk if !prev_chunk, else of the last)
+        if (tp == 0) return PW;
+        if (tp == 4 || tp == 6 || tp == 8) return (prev_chunk ? true : same_chunk_more) ? PW : 0;
+        return 0;
+      };
+      if constexpr (S == 2) {
+        const int n = T == 0 ? (c > 0 ? img(TP1, more, true) : 0) : img(TP1, more, false);
+        if (n) vm_wait<PW>(); else vm_wait<0>();
+      } else {
+        const int n1 = T == 0 ? (c > 0 ? img(TP1, more, true) : 0) : img(TP1, more, false);
+        const int n2 = T <= 1 ? (c > 0 ? img(TP2, more, true) : 0) : img(TP2, more, false);
+        const int n = n1 + n2;
+        if (n == 2 * PW) vm_wait<BW + 2 * PW>();
+        else if (n == PW) vm_wait<BW + PW>();
+        else vm_wait<BW>();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int T2 = (T + S - 1) % 9, C2 = (T + S - 1) / 9;
+      const int slot_new = slot == 0 ? S - 1 : slot - 1;  // (s + S - 1) % S
+      issue_b(c + C2, S2_ORDER[T2], slot_new);
+      if constexpr (T == 0) issue_sub(c, 3);
+      if constexpr (T == 4) { if (more) issue_sub(c + 1, 0); }
+      if constexpr (T == 6) { if (more) issue_sub(c + 1, 1); }
+      if constexpr (T == 8) { if (more) issue_sub(c + 1, 2); }
+      constexpr int TAP = S2_ORDER[T];
+      bf16x8 a[MT], b[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a[i] = *reinterpret_cast<const bf16x8*>(smem + aaddr[TAP][i]);
+      const char* bs = smem + b_rd + slot * B_STAGE;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(bs + j * 1024);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      slot = slot + 1 == S ? 0 : slot + 1;
+    });
+  }
+  vm_wait<0>();  // the past-the-end B fetches land before the block's LDS is released
+
+  // epilogue (conv_patch_bf16's LDS-staged stores): acc[i][j] = channels n0 + 16 j + 4 q .. + 3 of
+  // block voxel 16 (MT wid + i) + l16
+  const __bf16* res = reinterpret_cast<const __bf16*>(p.res);
+  __bf16* y = reinterpret_cast<__bf16*>(p.y);
+  auto finish = [&](int i, int j, size_t gm) __attribute__((always_inline)) {
+    const int n = n0 + j * 16 + 4 * q;
+    f32x4 v = acc[i][j] + *reinterpret_cast<const f32x4*>(p.bias + n);
+    if constexpr (EF & 1) {
+      const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + gm * p.Cout + n);
+      v += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
+    }
+    if constexpr (EF & 2) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = relu1(v[e]);
+    }
+    return bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  };
+  constexpr int SEG = NT * 32, VS = SEG + 16;
+  constexpr int MH = 4 * 16 * MT * VS <= LDS ? MT : 1, INS = 16 * MH * SEG / 1024;
+  static_assert(4 * 16 * MH * VS <= LDS, "staging fits the block's LDS");
+  static_assert(16 * MH * SEG % 1024 == 0, "whole store instructions");
+  char* st = smem + wid * 16 * MH * VS;
+  __builtin_amdgcn_s_barrier();  // every wave is past its last patch / weight read
+#pragma unroll
+  for (int i0 = 0; i0 < MT; i0 += MH) {
+#pragma unroll
+    for (int i = i0; i < i0 + MH; ++i) {
+      size_t gm = 0;
+      if constexpr (EF & 1) {
+        const int m = 16 * (MT * wid + i) + l16, f = m >> 6, px = m & 63, to = t0 + f;
+        const int ho = h0 + (px >> 3), wo = w0 + (px & 7);
+        gm = (((size_t)clip * p.To + (to < p.To ? to : 0)) * p.Ho + (ho < p.Ho ? ho : 0)) * p.Wo + (wo < p.Wo ? wo : 0);
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        *reinterpret_cast<bf16x4*>(st + (16 * (i - i0) + l16) * VS + (16 * j + 4 * q) * 2) = finish(i, j, gm);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    const int mp = 16 * (MT * wid + i0), f = mp >> 6, px0 = mp & 63, to = t0 + f;
+    __bf16* yb = y + ((((size_t)clip * p.To + to) * p.Ho + h0 + px0 / 8) * p.Wo + w0) * p.Cout + n0;
+    const bool full = to < p.To && h0 + px0 / 8 + 2 * MH <= p.Ho && w0 + 8 <= p.Wo;
+    const int row_el = p.Wo * p.Cout;
+#pragma unroll
+    for (int k = 0; k < INS; ++k) {
+      const int e = 1024 * k + 16 * lane, v = e / SEG, off = e - v * SEG;
+      const bf16x8 val = *reinterpret_cast<const bf16x8*>(st + v * VS + off);
+      const int lo = (v >> 3) * row_el + (v & 7) * p.Cout + off / 2;
+      if (full || (to < p.To && h0 + px0 / 8 + (v >> 3) < p.Ho && w0 + (v & 7) < p.Wo))
+        *reinterpret_cast<bf16x8*>(yb + lo) = val;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+  }
+}
+
+template <int NT, int FR, int S>
+constexpr int s2_occ() {
+  constexpr int lds = S2Geo<FR>::BYTES + S * NT * 1024 + 1024;
+  constexpr int occ = 160 * 1024 / lds;
+  return occ > 4 ? 4 : occ;
+}
+
+struct S2Grid {
+  int ptw, npt, tt;
+  long base;  // blocks per n tile
+};
+
+S2Grid s2_grid(const ConvParams& p, int fr) {
+  S2Grid g{};
+  g.ptw = (p.Wo + 7) / 8;
+  g.npt = g.ptw * ((p.Ho + 7) / 8);
+  g.tt = (p.To + fr - 1) / fr;
+  g.base = (long)p.N * g.tt * g.npt;
+  return g;
+}
+
+template <int NT, int FR, int S, int EF>
+hipError_t launch_s2_e(const ConvParams& p, hipStream_t s) {
+  const S2Grid g = s2_grid(p, FR);
+  const int n_tiles = p.Cout / (16 * NT);
+  hipLaunchKernelGGL((conv_patch_s2_bf16<NT, FR, S, s2_occ<NT, FR, S>(), EF>), dim3((unsigned)(g.base * n_tiles)),
+                     dim3(256), 0, s, p, n_tiles, g.ptw, g.npt, g.tt);
+  return hipGetLastError();
+}
+
+template <int NT, int FR = 2, int S = 2>
+hipError_t launch_s2(const ConvParams& p, hipStream_t s) {
+  switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
+    case 0: return launch_s2_e<NT, FR, S, 0>(p, s);
+    case 1: return launch_s2_e<NT, FR, S, 1>(p, s);
+    case 2: return launch_s2_e<NT, FR, S, 2>(p, s);
+    default: return launch_s2_e<NT, FR, S, 3>(p, s);
+  }
+}
+
+// N tile: the widest dividing Cout/16 with about two blocks per CU (>= 512 blocks); small grids take the
+// tile minimising ceil(blocks / 512) x (NT + 2) (two resident blocks per CU), as patch_pick_nt.
+// Per-clip shape rule: the choice depends on the batch only through the block count, and every NT runs
+// the same per-voxel products in the same order (bit-identical across NT).
+int s2_pick_nt(const ConvParams& p, int force_nt) {
+  const int n16 = p.Cout / 16;
+  const long base = s2_grid(p, 2).base;
+  int pick = 0;
+  for (int nt : {10, 8, 6, 5, 4}) {
+    if (n16 % nt) continue;
+    if (force_nt > 0) {
+      if (nt == force_nt) return nt;
+      continue;
+    }
+    if (!pick) pick = nt;
+    if (base * (n16 / nt) >= 512) return nt;
+  }
+  if (!pick || force_nt > 0) return 0;
+  long best = -1;
+  for (int nt : {10, 8, 6, 5, 4}) {
+    if (n16 % nt) continue;
+    const long cost = (base * (n16 / nt) + 511) / 512 * (nt + 2);
+    if (best < 0 || cost < best) best = cost, pick = nt;
+  }
+  return pick;
+}
+
+}  // namespace
+
+bool patch_s2_bf16_supported(const ConvParams& p) {
+  if (!p.in_bf16 || !p.out_bf16 || p.stem || p.x2 || !p.bias) return false;
+  if (!(p.KT == 1 && p.KH == 3 && p.KW == 3 && p.st == 1 && p.sh == 2 && p.sw == 2 && p.pt == 0 && p.ph == 1 && p.pw == 1))
+    return false;
+  if (p.Cin % 32 || p.Cout % 16 || p.Kp != 9 * p.Cin) return false;
+  if (p.To != p.Ti || p.Ho != (p.Hi + 1) / 2 || p.Wo != (p.Wi + 1) / 2) return false;
+  if (s2_pick_nt(p, p.patch_nt) == 0) return false;
+  if ((long)p.N * p.Ti * p.Hi * p.Wi >= (1L << 31) / 2) return false;
+  return true;
+}
+
+hipError_t launch_patch_s2_bf16(const ConvParams& p, hipStream_t s) {
+  if (!patch_s2_bf16_supported(p)) return hipErrorInvalidValue;
+  switch (s2_pick_nt(p, p.patch_nt)) {
+    case 10: return launch_s2<10>(p, s);
+    case 8: return launch_s2<8>(p, s);
+    case 6: return launch_s2<6>(p, s);
+    case 5: return launch_s2<5>(p, s);
+    case 4: return launch_s2<4>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+// tools/convbench: ko = S * 100 + FR * 10 (+ NT forced through CLASFV_PATCH_NT / CB patch_nt)
+hipError_t launch_patch_s2_bf16_ko(const ConvParams& p, hipStream_t s, int ko) {
+  if (!patch_s2_bf16_supported(p)) return hipErrorInvalidValue;
+  const int nt = s2_pick_nt(p, p.patch_nt), st = ko / 100, fr = ko / 10 % 10;
+  auto go = [&](auto ntc) -> hipError_t {
+    constexpr int NT = decltype(ntc)::value;
+    if (st == 3 && fr == 2) return launch_s2<NT, 2, 3>(p, s);
+    if constexpr (NT % 2 == 0) {  // FR 1: one m tile per wave (whole staged store instructions need even NT)
+      if (st == 2 && fr == 1) return launch_s2<NT, 1, 2>(p, s);
+      if (st == 3 && fr == 1) return launch_s2<NT, 1, 3>(p, s);
+    }
+    if (fr == 1) return hipErrorInvalidValue;
+    return launch_s2<NT, 2, 2>(p, s);
+  };
+  switch (nt) {
+    case 10: return go(std::integral_constant<int, 10>{});
+    case 8: return go(std::integral_constant<int, 8>{});
+    case 6: return go(std::integral_constant<int, 6>{});
+    case 5: return go(std::integral_constant<int, 5>{});
+    case 4: return go(std::integral_constant<int, 4>{});
+  }
+  return hipErrorInvalidValue;
+}
+#endif  // CLASFV_KNOCKOUTS
+
 bool patch_bf16_supported(const ConvParams& p) {
   if (!p.in_bf16 || !p.out_bf16 || p.stem || p.x2) return false;
   if (p.st != 1 || p.sh != 1 || p.sw != 1) return false;

@@ -29,6 +29,7 @@ hipError_t launch_dma_bf16_ko(const ConvParams& p, int bn, int ko, hipStream_t s
 hipError_t launch_patch_bf16_v1(const ConvParams& p, hipStream_t s);
 hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_patch32_bf16_epi(const ConvParams& p, hipStream_t s, int epi);
+hipError_t launch_patch_s2_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_winoq_probe(const ConvParams& p, hipStream_t s, int ko);
 void winos_stamps(unsigned long long* out);
 void wino4w_stamps(unsigned long long* out, int n);
@@ -198,6 +199,10 @@ int main(int argc, char** argv) {
       if (getenv("CB_MT")) mt = atoi(getenv("CB_MT"));
       ConvParams q = p;
       if (ko >= 700 && ko < 709) q.n_split = ko - 700;  // conv_dma split-K into ko - 700 K ranges
+      if (bf && ko >= 8000 && ko < 8400) {  // conv_patch_s2_bf16 (CB_STRIDE=2): ko - 8000 = S*100 + FR*10
+        CK(launch_patch_s2_bf16_ko(q, s, ko - 8000));
+        return;
+      }
       if (bf && ko >= 7300 && ko < 7402) {  // conv_dma bf16 knock-outs (KO = ko - 7300; + 1 the pointer DMAs); 7400 / 7401: conv_dma_w, 2 / 3 stages
         CK(launch_dma_bf16_ko(q, bn, ko - 7300, s));
         return;
