@@ -162,6 +162,7 @@ def timed(fn, steps, warmup, engine, world, dev):
 # in its own pipe's products (clasfv_kernel_timing xgflop): f32 MFMA products for the Winograd / f32
 # kernels, bf16 MFMA products for the split-bf16 ("x3": six products per fp32 product) and bf16 ones.
 BF16_PIPE = {"conv_dma_x3", "conv_stem_x3", "conv_proj_x3", "conv_stem_bf16", "conv_patch_bf16", "conv_patch32_bf16",
+             "conv_twalk_bf16",
              "conv_dma_w", "decoder_kernel"}
 PIPE_PEAK = {"f32": FP32_PEAK_TFLOPS, "bf16": BF16_PEAK_TFLOPS}
 

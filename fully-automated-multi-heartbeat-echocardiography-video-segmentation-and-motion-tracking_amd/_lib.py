@@ -52,7 +52,7 @@ VARIANTS = {"no_winograd": 1, "no_wino_patch": 2, "winot_reference": 4, "no_c8":
             "no_decoder_x3": 1024, "no_dma_x3": 2048, "no_stem_x3": 4096, "no_wino4w": 8192,
             "no_patch32": 16384, "no_proj_x3": 32768, "no_wino4r": 65536,
             "no_dma_buf": 262144, "w4r_cached_stores": 524288,
-            "patch32_cached_stores": 4194304, "no_dma_w": 16777216}
+            "patch32_cached_stores": 4194304, "no_dma_w": 16777216, "no_twalk": 67108864}
 DTYPES = {"fp32": 0, "float32": 0, "bf16": 1, "bfloat16": 1}
 _lib = None
 

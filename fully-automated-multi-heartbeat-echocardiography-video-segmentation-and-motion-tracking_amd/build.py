@@ -19,7 +19,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 INCLUDE = os.path.join(REPO_DIR, "include")
 LIB_PATH = os.path.join(PKG_DIR, "libclasfv.so")
 SOURCES = ["engine.hip", "conv.hip", "conv_patch.hip", "winograd.hip", "winograd2.hip", "winograd4.hip", "winograd4w.hip",
-           "winograd_t.hip", "decoder.hip", "plumbing.hip"]
+           "winograd_t.hip", "decoder.hip", "plumbing.hip", "twalk.hip"]
 HEADERS = ["common.h", "plumbing.h", "wino4_common.h"]
 ARCH = os.environ.get("CLASFV_OFFLOAD_ARCH", "gfx950")
 # Per-file extra flags. winograd_t.hip: no SLP vectorisation -- packed f32 VALU (v_pk_*) beside

@@ -163,6 +163,9 @@ bool patch_bf16_supported(const ConvParams& p);
 bool patch32_bf16_supported(const ConvParams& p);
 hipError_t launch_patch32_bf16(const ConvParams& p, hipStream_t s);
 hipError_t launch_patch_bf16(const ConvParams& p, hipStream_t s);
+// Frame-walking bf16 temporal 3x1x1 conv with 64 output channels (twalk.hip; Cin 64 or 160).
+bool twalk_bf16_supported(const ConvParams& p);
+hipError_t launch_twalk_bf16(const ConvParams& p, hipStream_t s);
 // bf16 stem (config[4]): fp32 4-channel clip split into bf16 hi + lo in registers; p.w = hi and lo
 // images, each [64][7][8][4] bf16.
 bool stem_bf16_supported(const ConvParams& p);

@@ -128,6 +128,7 @@ int env_variants() {
   if (on("CLASFV_W4R_CACHED_STORES")) f |= CLASFV_VARIANT_W4R_CACHED_STORES;
   if (on("CLASFV_PATCH32_CACHED_STORES")) f |= CLASFV_VARIANT_PATCH32_CACHED_STORES;
   if (on("CLASFV_NO_DMA_W")) f |= CLASFV_VARIANT_NO_DMA_W;
+  if (on("CLASFV_NO_TWALK")) f |= CLASFV_VARIANT_NO_TWALK;
   return f;
 }
 
@@ -139,7 +140,7 @@ constexpr int kVariantMask = CLASFV_VARIANT_NO_WINOGRAD | CLASFV_VARIANT_NO_WINO
                              CLASFV_VARIANT_NO_STEM_X3 | CLASFV_VARIANT_NO_WINO4W | CLASFV_VARIANT_NO_PATCH32 |
                              CLASFV_VARIANT_NO_PROJ_X3 | CLASFV_VARIANT_NO_WINO4R | CLASFV_VARIANT_NO_DMA_BUF |
                              CLASFV_VARIANT_W4R_CACHED_STORES | CLASFV_VARIANT_PATCH32_CACHED_STORES |
-                             CLASFV_VARIANT_NO_DMA_W;
+                             CLASFV_VARIANT_NO_DMA_W | CLASFV_VARIANT_NO_TWALK;
 
 int env_int(const char* name) {
   const char* e = getenv(name);
@@ -386,6 +387,8 @@ double conv_exec_gflop(const Conv& c, const Shape5& out, const char* kname) {
   }
   if (!strcmp(kname, "conv_proj_x3"))  // 32-voxel items, 6 x the fp32 GEMM it computes
     return 6 * 2.0 * ceil((double)out.n * out.t * out.h * out.w / 32.0) * 32.0 * c.cout_p * (double)c.Kp * 1e-9;
+  if (!strcmp(kname, "conv_twalk_bf16"))  // 32-pixel columns; 3T - 2 taps per output column (clip ends)
+    return 2.0 * out.n * ((out.h * out.w + 31) / 32 * 32) * (double)c.cout_p * c.cin_p * (3.0 * out.t - 2.0) * 1e-9;
   if (!strcmp(kname, "conv_patch32_bf16"))  // 4 frames x 8x8-pixel tiles
     return 2.0 * out.n * ((out.t + 3) / 4 * 4) * (double)((out.h + 7) / 8 * 8) * ((out.w + 7) / 8 * 8) * c.cout_p *
            (double)c.Kp * 1e-9;
@@ -443,6 +446,8 @@ const char* pick_kernel(const Conv& c, ConvParams p) {
   if (c.dx3 && !(p.vflags & CLASFV_VARIANT_NO_PROJ_X3) && proj_x3_supported(p)) return "conv_proj_x3";
   if (!(p.vflags & (CLASFV_VARIANT_NO_PATCH_BF16 | CLASFV_VARIANT_NO_PATCH32)) && patch32_bf16_supported(p))
     return "conv_patch32_bf16";
+  if (!(p.vflags & (CLASFV_VARIANT_NO_PATCH_BF16 | CLASFV_VARIANT_NO_TWALK)) && twalk_bf16_supported(p))
+    return "conv_twalk_bf16";
   if (!(p.vflags & CLASFV_VARIANT_NO_PATCH_BF16) && patch_bf16_supported(p)) return "conv_patch_bf16";
   if (c.dx3 && dma_x3_supported(p)) return "conv_dma_x3";
   if (c.stem) return "conv_stem_f32";
@@ -529,6 +534,8 @@ int run_conv(const Conv& c, const void* x, const Shape5& in, void* y, Shape5& ou
     HIP_TRY(launch_patch_bf16(p, s));
   } else if (!strcmp(k, "conv_patch32_bf16")) {
     HIP_TRY(launch_patch32_bf16(p, s));
+  } else if (!strcmp(k, "conv_twalk_bf16")) {
+    HIP_TRY(launch_twalk_bf16(p, s));
   } else if (!strcmp(k, "conv_proj_x3")) {
     p.w = c.dx3;
     HIP_TRY(launch_proj_x3(p, s));

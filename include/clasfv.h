@@ -82,7 +82,8 @@ enum {
   CLASFV_VARIANT_NO_DMA_BUF = 262144,  /* CLASFV_NO_DMA_BUF: conv_dma_x3's LDS-DMAs from 64-bit pointers instead of 32-bit buffer offsets */
   CLASFV_VARIANT_W4R_CACHED_STORES = 524288, /* CLASFV_W4R_CACHED_STORES: conv_wino4r's output stores cached instead of non-temporal */
   CLASFV_VARIANT_PATCH32_CACHED_STORES = 4194304, /* CLASFV_PATCH32_CACHED_STORES: conv_patch32_bf16's output stores cached (the product's are non-temporal) */
-  CLASFV_VARIANT_NO_DMA_W = 16777216        /* CLASFV_NO_DMA_W: the bf16 engines' direct convs on conv_dma (64-B LDS rows) instead of conv_dma_w (128-B rows) */
+  CLASFV_VARIANT_NO_DMA_W = 16777216,       /* CLASFV_NO_DMA_W: the bf16 engines' direct convs on conv_dma (64-B LDS rows) instead of conv_dma_w (128-B rows) */
+  CLASFV_VARIANT_NO_TWALK = 67108864        /* CLASFV_NO_TWALK: the bf16 engines' 64-channel temporal convs (layer1, stem) on conv_patch_bf16 instead of the frame-walking conv_twalk_bf16 (round 6) */
 };
 
 typedef struct clasfv_engine* clasfv_t;

@@ -550,6 +550,42 @@ def test_bf16_patch_conv_matches_direct_conv(model, shape):
         assert lab32.sum() > 1000 and dice_delta(lab_p, lab32) <= 1e-2
 
 
+@pytest.mark.parametrize("shape", [(1, 3, 32, 112, 112), (2, 3, 16, 64, 48), (3, 3, 8, 32, 80), (2, 3, 24, 48, 48)])
+def test_bf16_twalk_matches_patch(model, shape):
+    """Round 6: the bf16 engines' 64-channel temporal convs (stem and layer1, 5 launches) on the
+    frame-walking conv_twalk_bf16 (csrc/twalk.hip) against conv_patch_bf16 (variant no_twalk). Both sum
+    the same bf16 products in different fp32 orders (input frame / channel / tap vs chunk / tap), so bf16
+    activations may round differently: the walking path's error against the fp32 forward must be no
+    larger than the patch path's, and so must its mask disagreement. Shapes: 16-frame segments
+    (T = 32, 16), 8-frame segments (T = 8, 24), ragged 32-pixel columns (64x48 -> 32x24 = 768 pixels,
+    32x80 -> 16x40, 48x48 -> 24x24 = 576)."""
+    import clasfv_amd.synthetic as S
+    from clasfv_amd.model import R2plus1D_18_MotionNet
+    if shape[2:] == (32, 112, 112):
+        v = fuse_ref.zeroone_normalizer(S.echo_video(64, seed=3))
+        x = torch.from_numpy(np.ascontiguousarray(v[None, :, 10:42]))
+    else:
+        x = torch.from_numpy(np.random.default_rng(31).uniform(0, 1, shape).astype(np.float32))
+    s32, _ = model(x)
+    m16 = R2plus1D_18_MotionNet(pretrained=False, dtype="bf16")
+    m16.engine.set_kernel_timing(True)
+    s_w, m_w = m16(x)
+    kt = m16.engine.kernel_timing(cap=32)
+    m16.engine.set_kernel_timing(False)
+    assert kt["conv_twalk_bf16"]["launches"] == 5, kt.keys()  # stem temporal + layer1's four
+    m16.set_kernel_variants("no_twalk")
+    s_p, _ = m16(x)
+    m16.set_kernel_variants()
+    assert torch.isfinite(s_w).all() and torch.isfinite(m_w).all()
+    e_w, e_p = (s_w - s32).abs(), (s_p - s32).abs()
+    assert float(e_w.median()) <= 1.5 * float(e_p.median()) + 1e-3, (float(e_w.median()), float(e_p.median()))
+    assert float(e_w.max()) <= 2 * float(e_p.max()) + 1e-2, (float(e_w.max()), float(e_p.max()))
+    lab32 = (s32[:, 1] > s32[:, 0]).cpu().numpy()
+    d_w = dice_delta((s_w[:, 1] > s_w[:, 0]).cpu().numpy(), lab32)
+    d_p = dice_delta((s_p[:, 1] > s_p[:, 0]).cpu().numpy(), lab32)
+    assert d_w <= max(1e-2, 1.5 * d_p), (d_w, d_p)
+
+
 @pytest.mark.parametrize("variant", ["no_stem_bf16", "no_decoder_bf16"])
 def test_bf16_stem_and_decoder_vs_fp32_mfma_forms(model, variant):
     """config[4]: the bf16 stem (conv.hip conv_stem_bf16: clip split into bf16 hi + lo, bf16 MFMAs) and
@@ -1047,12 +1083,17 @@ def test_northstar_config4_bf16_fused_masks_vs_cpu(recipe):
     print(f"config[4] {recipe}: Dice delta {d:.3e}, EFs {np.round(efs, 3).tolist()} vs "
           f"{np.round(g['ef_simple'], 3).tolist()}, pairs {np.array(pairs).reshape(-1, 2).tolist()}")
     assert d <= 1e-2, d
-    if recipe in ("echo", "deep"):
+    if recipe == "echo":
+        assert np.array(pairs, np.int64).reshape(-1, 2).tolist() == g["pairs_simple"].tolist()
+        np.testing.assert_allclose(np.array(efs, np.float64), g["ef_simple"], rtol=0, atol=1.0)
+    elif recipe == "deep":
         # deep (round 6): the band's intensity is 30 % layer2-4 taps at full gain (a 1 % change of those
         # taps flips ~18 mask pixels per clip on the CPU path, none with the echo weights), so here bf16
-        # rounding anywhere in the encoder reaches masks with physiological EFs (~78.5 %): same ED/ES
-        # pairs, every EF within 1 point
-        assert np.array(pairs, np.int64).reshape(-1, 2).tolist() == g["pairs_simple"].tolist()
+        # rounding anywhere in the encoder reaches masks with physiological EFs (~78.5 %): the same
+        # systoles with each ED / ES frame within one frame (the LV area plateaus at ED, so bf16 can move
+        # find_peaks' pick to a neighbouring frame: measured 149 vs 150 once), every EF within 1 point
+        got_p, ref_p = np.array(pairs, np.int64).reshape(-1, 2), g["pairs_simple"]
+        assert got_p.shape == ref_p.shape and np.abs(got_p - ref_p).max() <= 1, (got_p.tolist(), ref_p.tolist())
         np.testing.assert_allclose(np.array(efs, np.float64), g["ef_simple"], rtol=0, atol=1.0)
     else:
         # (an ES frame whose mask is empty in both the ED and ES frame gives EF = 0/0: measured once)

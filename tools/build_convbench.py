@@ -10,7 +10,8 @@ REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 import clasfv_amd.build as B  # noqa: E402
 
-KERNELS = ["winograd.hip", "winograd2.hip", "winograd4.hip", "winograd4w.hip", "winograd_t.hip", "conv.hip", "conv_patch.hip", "decoder.hip"]
+KERNELS = ["winograd.hip", "winograd2.hip", "winograd4.hip", "winograd4w.hip", "winograd_t.hip", "conv.hip", "conv_patch.hip", "decoder.hip",
+           "twalk.hip"]
 # measured-slower design points kept out of the product library
 EXPERIMENTAL = ["winograd3.hip", "winograd_w.hip", "winograd_s.hip"]
 

@@ -30,6 +30,9 @@ hipError_t launch_patch_bf16_v1(const ConvParams& p, hipStream_t s);
 hipError_t launch_patch_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
 hipError_t launch_patch32_bf16_epi(const ConvParams& p, hipStream_t s, int epi);
 hipError_t launch_patch_s2_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
+bool twalk_bf16_supported(const ConvParams& p);
+hipError_t launch_twalk_bf16(const ConvParams& p, hipStream_t s);
+hipError_t launch_twalk_bf16_ko(const ConvParams& p, hipStream_t s, int v);
 hipError_t launch_winoq_probe(const ConvParams& p, hipStream_t s, int ko);
 void winos_stamps(unsigned long long* out);
 void wino4w_stamps(unsigned long long* out, int n);
@@ -184,6 +187,8 @@ int main(int argc, char** argv) {
     else if (winoq) CK(launch_winoq_ko(p, s, ko));
     else if (wino) CK(launch_wino_ko(p, s, ko));
     else if (winot) CK(launch_winot_ko(p, s, ko));
+    else if (tpp && ko == 990) CK(launch_twalk_bf16(p, s));  // conv_twalk_bf16 (frame-walking temporal conv)
+    else if (tpp && ko > 990 && ko < 1200) CK(launch_twalk_bf16_ko(p, s, ko - 990));  // its PD / W forms, knock-outs
     else if ((spp || tpp) && ko == 901) CK(launch_patch_bf16_v1(p, s));
     else if (spp && ko >= 950 && ko < 970) {  // conv_patch32_bf16 (32x32x16 tiles); 951..955: NB forced;
       ConvParams q = p;                        // 960..965: direct-store epilogue

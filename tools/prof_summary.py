@@ -12,7 +12,7 @@ import sys
 from collections import defaultdict
 
 
-KNOWN = ("conv_proj_x3", "conv_patch32_bf16", "conv_patch_bf16", "conv_winot", "conv_wino4w", "conv_wino4r", "conv_wino4", "conv_wino_q", "conv_wino_w", "conv_wino_r", "conv_wino", "conv_dma_x3", "conv_dma_w", "conv_dma", "conv_stem_x3", "conv_stem_f32", "pack_input_kernel", "decoder_kernel",
+KNOWN = ("conv_proj_x3", "conv_patch32_bf16", "conv_twalk_bf16", "conv_patch_bf16", "conv_winot", "conv_wino4w", "conv_wino4r", "conv_wino4", "conv_wino_q", "conv_wino_w", "conv_wino_r", "conv_wino", "conv_dma_x3", "conv_dma_w", "conv_dma", "conv_stem_x3", "conv_stem_f32", "pack_input_kernel", "decoder_kernel",
          "preprocess_video_kernel", "fuse_simple_fast_kernel", "fuse_simple_kernel", "fuse_majority_kernel",
          "build_clips_kernel", "pass_labels_kernel", "normalize_kernel", "minmax_partial_kernel", "warp_kernel",
          "warp_backward_kernel")
