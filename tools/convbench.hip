@@ -33,6 +33,9 @@ hipError_t launch_patch_s2_bf16_ko(const ConvParams& p, hipStream_t s, int ko);
 bool twalk_bf16_supported(const ConvParams& p);
 hipError_t launch_twalk_bf16(const ConvParams& p, hipStream_t s);
 hipError_t launch_twalk_bf16_ko(const ConvParams& p, hipStream_t s, int v);
+hipError_t launch_twalk_x3(const ConvParams& p, hipStream_t s);
+hipError_t launch_twalk_x3_ko(const ConvParams& p, hipStream_t s, int v);
+void twalk_x3_weight_image(const float* w, int cout, int kp, uint16_t* out);
 hipError_t launch_winoq_probe(const ConvParams& p, hipStream_t s, int ko);
 void winos_stamps(unsigned long long* out);
 void wino4w_stamps(unsigned long long* out, int n);
@@ -159,6 +162,18 @@ int main(int argc, char** argv) {
       CK(hipMalloc(&wx3, img.size() * 2));
       CK(hipMemcpy(wx3, img.data(), img.size() * 2, hipMemcpyHostToDevice));
     }
+  // ko 1300.. (winot shapes): conv_twalk_x3 (fp32 frame walk on split-bf16 MFMAs) on its piece image of
+  // random [Cout][3 Cin] weights
+  void* wtx = nullptr;
+  for (int ko : kos)
+    if (winot && ko >= 1300 && ko < 1310 && !wtx) {
+      std::vector<float> wf((size_t)Cout * 3 * Cin);
+      for (size_t i = 0; i < wf.size(); ++i) wf[i] = 0.1f * (float)((i * 2654435761u) % 1000) / 1000.f - 0.05f;
+      std::vector<uint16_t> img(3 * wf.size());
+      twalk_x3_weight_image(wf.data(), Cout, 3 * Cin, img.data());
+      CK(hipMalloc(&wtx, img.size() * 2));
+      CK(hipMemcpy(wtx, img.data(), img.size() * 2, hipMemcpyHostToDevice));
+    }
   for (int ko : kos)
     if (((winot && ko >= 600 && ko < 700) || (!wino && !winot && ko >= 700 && ko < 720)) && !p.part)
       CK(hipMalloc((void**)&p.part, 8 * ny * 4));  // split-K partials
@@ -186,7 +201,12 @@ int main(int argc, char** argv) {
     else if (winoqp) CK(launch_winoq_probe(p, s, ko));
     else if (winoq) CK(launch_winoq_ko(p, s, ko));
     else if (wino) CK(launch_wino_ko(p, s, ko));
-    else if (winot) CK(launch_winot_ko(p, s, ko));
+    else if (winot && ko >= 1300 && ko < 1310) {  // 1300 product, 1300 + v: waves per SIMD v
+      ConvParams q = p;
+      q.w = wtx;
+      q.Kp = 3 * Cin;
+      CK(ko == 1300 ? launch_twalk_x3(q, s) : launch_twalk_x3_ko(q, s, ko - 1300));
+    } else if (winot) CK(launch_winot_ko(p, s, ko));
     else if (tpp && ko == 990) CK(launch_twalk_bf16(p, s));  // conv_twalk_bf16 (frame-walking temporal conv)
     else if (tpp && ko > 990 && ko < 1200) CK(launch_twalk_bf16_ko(p, s, ko - 990));  // its PD / W forms, knock-outs
     else if ((spp || tpp) && ko == 901) CK(launch_patch_bf16_v1(p, s));

@@ -1,8 +1,8 @@
 #!/bin/bash
-# bf16 config[4] bench A/B: ENV_A vs ENV_B (environment assignments, e.g. "CLASFV_NO_TWALK=1"), interleaved
+# bf16 config[4] (DTYPE=fp32: the fp32 headline) bench A/B: ENV_A vs ENV_B (environment assignments, e.g. "CLASFV_NO_TWALK=1"), interleaved
 # A B A B, each a fresh process; prints value, ms/step and the per-kernel summed ms
 out=${1:-gpurun_out/ab_bf16}; A=${2:-}; B=${3:-}; mkdir -p $out; export TMPDIR=/tmp
-BA="bench.py --dtype bf16 --extra-bf16 0 --extra-c3 0 --extra-stream 0 --cpu-baseline 0 --parity-random 0 --steps 20 --warmup 3"
+BA="bench.py --dtype ${DTYPE:-bf16} --extra-bf16 0 --extra-c3 0 --extra-stream 0 --cpu-baseline 0 --parity-random 0 --steps 20 --warmup 3"
 i=0
 for v in A B A B; do
   i=$((i+1)); E=$A; [ $v = B ] && E=$B
