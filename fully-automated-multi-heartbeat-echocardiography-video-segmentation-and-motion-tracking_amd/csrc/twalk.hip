@@ -32,6 +32,7 @@
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int tw_u32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
 
   // this wave's (clip, 32-pixel column, frame segment)
   const int HW = p.Hi * p.Wi, T = p.Ti;
-  int item = blockIdx.x * 4 + (tid >> 6);
+  int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (tid >> 6));  // wave-uniform: scalar
   const int seg = item % n_seg;
   item /= n_seg;
   const int col = item % n_cols, clip = item / n_cols;
@@ -101,13 +102,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
 
+  // Every load is issued on every path -- a frame outside the clip (zero padding) reads the clip's end
+  // frame and is zeroed before use (segment end steps only) -- so each wait counts exactly the memory
+  // operations issued after the ones it needs (a conditional load made the compiler wait for the next
+  // frame's loads too: vmcnt(9) .. vmcnt(5) in every step).
   auto load_frame = [&](int u, bf16x8 (&dst)[CS]) __attribute__((always_inline)) {
     if ((KO & 2) && u > ta + 1) return;
-    if (u >= 0 && u < T) {  // wave-uniform; frames outside the clip are zero padding (never read)
-      const __bf16* src = x + (size_t)u * frame_x;
+    const int uc = u < 0 ? 0 : u >= T ? T - 1 : u;
+    const __bf16* src = x + (size_t)uc * frame_x;
 #pragma unroll
-      for (int s = 0; s < CS; ++s) dst[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
-    }
+    for (int s = 0; s < CS; ++s) dst[s] = *reinterpret_cast<const bf16x8*>(src + 16 * s);
   };
   // A fragment (weights) of tap kt, 16-channel step s, row block rb: row 32 rb + r, k 16 s + 8 h
   const char* wa = smem + r * PITCH + (8 * h) * 2;
@@ -122,15 +126,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
   // moves 8 whole 128-B pixel rows (lane: row 8 k + lane / 8, 16-B slot lane % 8) instead of 8-B pieces
   // of 32 rows. The residual of output frame o is loaded one step before its epilogue (double-buffered,
   // 4 x 16 B per lane).
+  // Rows past the map: buffer resources over the column's valid rows (reads return zeros, stores are
+  // dropped), no per-lane branches.
   f32x4 rvq[2][4];
+  const int col_bytes = (HW - col * TW_PX < TW_PX ? HW - col * TW_PX : TW_PX) * 128;
+  const int row_off = (lane >> 3) * 128 + (lane & 7) * 16;
   auto load_res = [&](int o, f32x4 (&rq)[4]) __attribute__((always_inline)) {
     if constexpr (EF & 1) {
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<__bf16*>(rbase + (size_t)o * frame_y), (short)0, col_bytes, 0x00020000);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int row = 8 * k + (lane >> 3), sl = lane & 7;
-        rq[k] = col * TW_PX + row < HW ? *reinterpret_cast<const f32x4*>(rbase + (size_t)o * frame_y + (size_t)row * 64 + sl * 8)
-                                       : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      for (int k = 0; k < 4; ++k)
+        rq[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, row_off + k * 1024, 0, 0));
     }
   };
   auto wave_sync = [&]() __attribute__((always_inline)) {
@@ -172,11 +179,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
       }
     if constexpr (!(KO & 1)) {
       wave_sync();
+      const __amdgpu_buffer_rsrc_t yr =
+          __builtin_amdgcn_make_buffer_rsrc(ybase + (size_t)o * frame_y, (short)0, col_bytes, 0x00020000);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int row = 8 * k + (lane >> 3), sl = lane & 7;
         const f32x4 val = *reinterpret_cast<const f32x4*>(stg + row * TW_SP + sl * 16);
-        if (col * TW_PX + row < HW) *reinterpret_cast<f32x4*>(ybase + (size_t)o * frame_y + (size_t)row * 64 + sl * 8) = val;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tw_u32x4, val), yr, row_off + k * 1024, 0, 0);
       }
       wave_sync();
     }
@@ -190,13 +199,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
     const int u = ta - 1 + I;
     if constexpr (I + PD < NI) load_frame(u + PD, xr[(I + PD) % NR]);  // PD frames ahead
     if constexpr (I >= 1 && I <= TS) load_res(u, rvq[I % 2]);       // stored at step I + 1
-    if (u >= 0 && u < T) {
+    // only a segment's end steps can fall outside the clip: their frame is zeroed by a select (no branch)
+    constexpr bool EDGE = I == 0 || I == NI - 1;
+    const bool fv = u >= 0 && u < T;
+    {
       // contributions: tap 2 -> y[u - 1] (if u - 1 >= ta), tap 1 -> y[u] (if u < ta + TS), tap 0 -> y[u + 1]
       // (if u + 1 < ta + TS); the conditions are compile-time in I (ta is the segment start)
       constexpr bool T2 = I >= 2, T1 = I >= 1 && I <= TS, T0 = I <= TS - 1;
 #pragma unroll
       for (int s = 0; s < CS; ++s) {
-        const bf16x8 b = xr[SX][s];
+        bf16x8 b = xr[SX][s];
+        if constexpr (EDGE) b = fv ? b : bf16x8{};
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           if constexpr (KO & 4) {
