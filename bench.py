@@ -561,6 +561,7 @@ def run_c2(args, model, world, rank, dev):
         "rows_exchanged_per_step": main_run["rows_exchanged_per_step"],
         "bytes_exchanged_per_step": main_run["bytes_exchanged_per_step"],
         "exchange_ms_per_step": main_run["exchange_ms_per_step"],
+        "exchange_transfer_ms": main_run["exchange_transfer_ms"], "exchange_note": main_run["exchange_note"],
         "fuse_extra": extra, "lv_fraction": round(float(np.mean(sum(lv_all, []))), 4),
     }
 
