@@ -314,8 +314,16 @@ def northstar_parity(args, fused_video0, dtype, recipe=BENCH_WEIGHTS):
     else:
         ef_delta = mean_delta = None
     dice = float(1.0 - categorical_dice(got, ref, 1))
+    # when an ED / ES frame moved (a mask at the decision margin on one frame), the systoles still pair
+    # up by index: the largest frame shift and the EF deltas of the index-matched systoles
+    gp, rp = np.array(pairs, np.int64).reshape(-1, 2), np.asarray(g[f"pairs_{args.fuse_method}"]).reshape(-1, 2)
+    matched = None
+    if not same_pairs and len(gp) == len(rp) and len(efs):
+        d = np.abs(np.array(efs) - ref_ef)
+        matched = {"max_frame_shift": int(np.abs(gp - rp).max()),
+                   "ef_delta_max": float(np.nanmax(d)) if np.isfinite(d).any() else None}
     return {"dice_delta_fused_masks": round(dice, 9), "ef_delta_max_per_systole": ef_delta, "ef_delta_mean": mean_delta,
-            "ed_es_pairs_equal": same_pairs, "bar": DICE_BAR[dtype], "within_bar": dice <= DICE_BAR[dtype],
+            "ed_es_pairs_equal": same_pairs, "index_matched_systoles": matched, "bar": DICE_BAR[dtype], "within_bar": dice <= DICE_BAR[dtype],
             "efs_gpu": [round(float(e), 4) for e in efs], "efs_cpu": [round(float(e), 4) for e in ref_ef],
             "weights": recipe,
             "reference": "tests/golden/%s (oracle CPU path, same video and weights, fuse=%s)"

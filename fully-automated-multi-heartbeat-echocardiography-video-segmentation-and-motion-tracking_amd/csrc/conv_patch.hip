@@ -750,9 +750,10 @@ hipError_t launch_p32(const ConvParams& p, hipStream_t s) {
 // layer3 576 at NB 3 0.152 vs 0.156, layer4 1152 at NB 2 0.114 vs 0.088). 0: not taken. force_nb > 0
 // (convbench, CLASFV_PATCH_NT = -NB) takes any NB that divides.
 // The rule counts blocks per clip, never the batch's, so whether a clip's layer1 runs 32x32x16 or
-// 16x16x32 products -- and so its rounding -- does not depend on how many clips share the launch. The
-// price is paid on small batches, where the r04 measurement found conv_patch_bf16 as fast or faster: a
-// deliberate determinism-over-speed trade (its cost at N = 1 and 4: profiles/r06*_patch32_small_batch.txt).
+// 16x16x32 products -- and so its rounding -- does not depend on how many clips share the launch. On
+// small batches it costs nothing: with the round-5 kernels conv_patch32_bf16 is the faster form at every
+// batch size (layer1, with the residual: N = 1 0.032 vs 0.044 ms, N = 4 0.105 vs 0.151, N = 30 0.756 vs
+// 1.013; profiles/r06j_patch32_small_batch.txt).
 int patch32_pick_nb(const ConvParams& p, int force_nb) {
   if (p.Cout % 32) return 0;
   const int n32 = p.Cout / 32;
