@@ -743,22 +743,27 @@ hipError_t launch_p32(const ConvParams& p, hipStream_t s) {
   }
 }
 
-// N tile (32-channel blocks). Product rule: NB = 5 (160-channel blocks: the bf16 layer1 spatial
-// convs, 64 -> 160) when ONE CLIP's map gives >= 128 blocks (every 112x112-clip layer1 map: 32x112x112
-// gives 392); everywhere else conv_patch_bf16 is as fast or faster (convbench, 30 clips,
-// profiles/r04_patch32_bf16.txt: layer1 0.686 vs 0.726 ms, layer2 288 channels at NB 3 0.325 vs 0.313,
-// layer3 576 at NB 3 0.152 vs 0.156, layer4 1152 at NB 2 0.114 vs 0.088). 0: not taken. force_nb > 0
-// (convbench, CLASFV_PATCH_NT = -NB) takes any NB that divides.
-// The rule counts blocks per clip, never the batch's, so whether a clip's layer1 runs 32x32x16 or
-// 16x16x32 products -- and so its rounding -- does not depend on how many clips share the launch. On
-// small batches it costs nothing: with the round-5 kernels conv_patch32_bf16 is the faster form at every
-// batch size (layer1, with the residual: N = 1 0.032 vs 0.044 ms, N = 4 0.105 vs 0.151, N = 30 0.756 vs
-// 1.013; profiles/r06j_patch32_small_batch.txt).
+// N tile (32-channel blocks). Product rule, per clip: the widest of NB = 5, 4, 3 (160-, 128-, 96-channel
+// blocks) that divides Cout / 32 and gives ONE CLIP >= 24 blocks -- layer1's 64 -> 160 (NB 5: 392 blocks
+// per 32x112x112 clip), layer2's 128 -> 256 (NB 4) and 128 -> 288 (NB 3), layer3's 256 -> 480 (NB 5) and
+// 256 -> 576 (NB 3); layer4's 7x7 maps give 9-12 and stay on conv_patch_bf16. Round 6 (convbench, 30
+// clips, profiles/r06k_patch32_layer234.txt): layer2 0.241 vs conv_patch_bf16's 0.268 ms (256) and 0.303
+// vs 0.307 (288), layer3 0.115 vs 0.126 (480) and 0.146 vs 0.155 (576), layer4 0.086 vs 0.082 (round 4
+// had found conv_patch_bf16 as fast or faster on layer2-4, before both kernels' store and DMA work);
+// bit-identical. 0: not taken. force_nb > 0 (convbench, CLASFV_PATCH_NT = -NB) takes any NB that divides.
+// The rule counts blocks per clip, never the batch's, so whether a clip's convs run 32x32x16 or
+// 16x16x32 products does not depend on how many clips share the launch (the two are bit-identical
+// anyway). On small batches it costs nothing: with the round-5 kernels conv_patch32_bf16 is the faster
+// form at every batch size (layer1, with the residual: N = 1 0.032 vs 0.044 ms, N = 4 0.105 vs 0.151,
+// N = 30 0.756 vs 1.013; profiles/r06j_patch32_small_batch.txt).
 int patch32_pick_nb(const ConvParams& p, int force_nb) {
   if (p.Cout % 32) return 0;
   const int n32 = p.Cout / 32;
   if (force_nb > 0) return (force_nb <= 5 && force_nb >= 2 && n32 % force_nb == 0) ? force_nb : 0;
-  return n32 % 5 == 0 && patch_grid(p, 4).base / p.N * (n32 / 5) >= 128 ? 5 : 0;
+  const long per_clip = patch_grid(p, 4).base / p.N;  // frame blocks x 8x8 tiles of one clip
+  for (int nb : {5, 4, 3})
+    if (n32 % nb == 0 && per_clip * (n32 / nb) >= 24) return nb;
+  return 0;
 }
 
 }  // namespace

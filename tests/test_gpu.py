@@ -721,11 +721,13 @@ def test_proj_x3_bitexact_vs_dma_x3(model, shape):
 
 @pytest.mark.parametrize("shape", [(2, 3, 32, 112, 112), (3, 3, 24, 80, 112)])
 def test_bf16_patch32_bitexact_vs_patch16(shape):
-    """config[4]: the bf16 layer1 spatial convs on conv_patch32_bf16 (v_mfma_f32_32x32x16_bf16, 4-frame
-    blocks, LDS-staged stores) against conv_patch_bf16 (16x16x32, 2-frame blocks; variant no_patch32):
-    the same bf16 products summed in fp32 -- bit-identical outputs on the box (convbench CB_CHECK over
-    4.8e8 layer1 outputs, profiles/r04_patch32_bf16.txt), asserted here on the whole forward (the
-    kernel takes grids of >= 512 blocks: 2 clips at 32x112x112; 3 clips with 40x56 layer1 maps)."""
+    """config[4]: the bf16 layer1 spatial convs (NB 5) and, since round 6, layer2's and layer3's
+    stride-1 spatial convs (NB 4 / 3 / 5 / 3 for 256 / 288 / 480 / 576 channels) on conv_patch32_bf16 (v_mfma_f32_32x32x16_bf16,
+    4-frame blocks, LDS-staged stores) against conv_patch_bf16 (16x16x32, 2-frame blocks; variant
+    no_patch32): the same bf16 products summed in fp32 -- bit-identical outputs on the box (convbench
+    CB_CHECK over 4.8e8 layer1 outputs, profiles/r04_patch32_bf16.txt; layer2/3: r06k), asserted here on
+    the whole forward: 10 launches (layer1's four, layer2's and layer3's three; layer4's 7x7 maps give
+    too few blocks per clip) at 32x112x112 and with 40x56 layer1 maps."""
     from clasfv_amd.model import R2plus1D_18_MotionNet
     rng = np.random.default_rng(53)
     x = torch.from_numpy(rng.uniform(0, 1, shape).astype(np.float32)).cuda()
@@ -734,7 +736,7 @@ def test_bf16_patch32_bitexact_vs_patch16(shape):
     s_32, mo_32 = m16(x)
     kt = m16.engine.kernel_timing()
     m16.engine.set_kernel_timing(False)
-    assert "conv_patch32_bf16" in kt
+    assert kt["conv_patch32_bf16"]["launches"] == 10, kt.keys()
     m16.set_kernel_variants("no_patch32")
     s_16, mo_16 = m16(x)
     m16.set_kernel_variants()
