@@ -48,10 +48,12 @@ __device__ inline void tw_unroll(std::integer_sequence<int, I...>, F&& f) {
 }
 
 // CS = Cin / 16 (16-channel K steps per tap), TS = output frames per wave segment, EF bit 0 residual,
-// bit 1 ReLU, PD = input frames loaded ahead (register ring of PD + 1 frames), W = waves per SIMD
+// bit 1 ReLU, PD = input frames loaded ahead (register ring of PD + 1 frames), W = waves per SIMD,
+// HV = 64-channel output halves (Cout = 64 HV; HV = 2: layer2's 128 channels, each block one half, the
+// two halves of a column on one XCD so the second reads the input frames from its L2)
 // KO (convbench knock-outs, wrong results): 1 no output stores, 2 no input loads in the walk, 4 no MFMAs
 constexpr int TW_SP = 144;  // staging row pitch (bytes): 128 + 16, conflict-free 8-B accesses of 32 rows
-template <int CS, int TS, int EF, int PD, int W, int KO = 0>
+template <int CS, int TS, int EF, int PD, int W, int KO = 0, int HV = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) void conv_twalk_bf16(ConvParams p, int n_cols,
                                                                                                    int n_seg) {
   constexpr int CIN = 16 * CS, KP = 3 * CIN, PITCH = tw_pitch(CIN);
@@ -62,22 +64,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
-  // weights -> LDS once per block (16-B chunks, row pitch PITCH)
+  // HV = 2: blocks 16 j + x (half 0) and 16 j + 8 + x (half 1) hold the same columns and run on XCD x
+  const int half = HV == 2 ? (blockIdx.x >> 3) & 1 : 0;
+  const int bpair = HV == 2 ? (blockIdx.x >> 4) * 8 + (blockIdx.x & 7) : blockIdx.x;
+  // weights -> LDS once per block (16-B chunks, row pitch PITCH): rows 64 half .. + 63
   {
-    const char* w = reinterpret_cast<const char*>(p.w);
+    const char* w = reinterpret_cast<const char*>(p.w) + (size_t)64 * half * KP * 2;
     constexpr int CPR = KP * 2 / 16;  // 16-B chunks per weight row
     for (int c = tid; c < 64 * CPR; c += 256) {
       const int row = c / CPR, k = c - row * CPR;
       *reinterpret_cast<f32x4*>(smem + row * PITCH + k * 16) =
           *reinterpret_cast<const f32x4*>(w + ((size_t)row * KP) * 2 + k * 16);
     }
-    if (tid < 64) sbias[tid] = p.bias[tid];
+    if (tid < 64) sbias[tid] = p.bias[64 * half + tid];
   }
   __syncthreads();
 
   // this wave's (clip, 32-pixel column, frame segment)
   const int HW = p.Hi * p.Wi, T = p.Ti;
-  int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (tid >> 6));  // wave-uniform: scalar
+  int item = __builtin_amdgcn_readfirstlane(bpair * 4 + (tid >> 6));  // wave-uniform: scalar
   const int seg = item % n_seg;
   item /= n_seg;
   const int col = item % n_cols, clip = item / n_cols;
@@ -87,10 +92,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
   const bool pv = px < HW;  // lanes past the map load pixel 0 (their outputs are not stored)
   const __bf16* x = reinterpret_cast<const __bf16*>(p.x) + ((size_t)clip * T * HW + (pv ? px : 0)) * CIN + 8 * h;
   const size_t frame_x = (size_t)HW * CIN;
-  // the column's pixel 0 in the output and the residual
-  __bf16* ybase = reinterpret_cast<__bf16*>(p.y) + ((size_t)clip * T * HW + col * TW_PX) * 64;
-  const __bf16* rbase = reinterpret_cast<const __bf16*>(p.res) + ((size_t)clip * T * HW + col * TW_PX) * 64;
-  const size_t frame_y = (size_t)HW * 64;
+  // the column's pixel 0 (this half's channel 0) in the output and the residual
+  constexpr int CO = 64 * HV;  // output channels = output pixel pitch (elements)
+  __bf16* ybase = reinterpret_cast<__bf16*>(p.y) + ((size_t)clip * T * HW + col * TW_PX) * CO + 64 * half;
+  const __bf16* rbase = reinterpret_cast<const __bf16*>(p.res) + ((size_t)clip * T * HW + col * TW_PX) * CO + 64 * half;
+  const size_t frame_y = (size_t)HW * CO;
 
   constexpr int NR = PD + 1;
   bf16x8 xr[NR][CS];  // register ring: input frame ta - 1 + i in slot i % NR
@@ -129,15 +135,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
   // Rows past the map: buffer resources over the column's valid rows (reads return zeros, stores are
   // dropped), no per-lane branches.
   f32x4 rvq[2][4];
-  const int col_bytes = (HW - col * TW_PX < TW_PX ? HW - col * TW_PX : TW_PX) * 128;
-  const int row_off = (lane >> 3) * 128 + (lane & 7) * 16;
+  const int col_bytes = (HW - col * TW_PX < TW_PX ? HW - col * TW_PX : TW_PX) * 2 * CO;
+  const int row_off = (lane >> 3) * 2 * CO + (lane & 7) * 16;
   auto load_res = [&](int o, f32x4 (&rq)[4]) __attribute__((always_inline)) {
     if constexpr (EF & 1) {
       const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
           const_cast<__bf16*>(rbase + (size_t)o * frame_y), (short)0, col_bytes, 0x00020000);
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        rq[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, row_off + k * 1024, 0, 0));
+        rq[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, row_off + k * 16 * CO, 0, 0));
     }
   };
   auto wave_sync = [&]() __attribute__((always_inline)) {
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W, W))) voi
       for (int k = 0; k < 4; ++k) {
         const int row = 8 * k + (lane >> 3), sl = lane & 7;
         const f32x4 val = *reinterpret_cast<const f32x4*>(stg + row * TW_SP + sl * 16);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tw_u32x4, val), yr, row_off + k * 1024, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(tw_u32x4, val), yr, row_off + k * 16 * CO, 0, 0);
       }
       wave_sync();
     }
@@ -232,41 +238,55 @@ bool twalk_bf16_supported(const ConvParams& p) {
   if (!p.in_bf16 || !p.out_bf16 || p.stem || p.x2 || !p.bias || p.x_c8 || p.y_c8) return false;
   if (!(p.KT == 3 && p.KH == 1 && p.KW == 1 && p.st == 1 && p.sh == 1 && p.sw == 1 && p.pt == 1 && p.ph == 0 && p.pw == 0))
     return false;
-  if (p.Cout != 64 || !(p.Cin == 160 || p.Cin == 64) || p.Kp != 3 * p.Cin) return false;
+  if (p.Kp != 3 * p.Cin) return false;
+  // 64 output channels: the stem's and layer1's (Cin 64, 160). convbench builds also take layer2's 128
+  // (Cin 256, 288; two 64-channel halves per column): measured and not taken by the product -- 0.138 /
+  // 0.116 ms vs conv_patch_bf16's 0.110 / 0.096 without the residual, 0.145 / 0.126 vs 0.153 / 0.141 with
+  // it (8-frame segments; profiles/r06l_twalk_layer2.txt)
+#ifdef CLASFV_KNOCKOUTS
+  if (!((p.Cout == 64 && (p.Cin == 160 || p.Cin == 64)) || (p.Cout == 128 && (p.Cin == 256 || p.Cin == 288))))
+    return false;
+#else
+  if (!(p.Cout == 64 && (p.Cin == 160 || p.Cin == 64))) return false;
+#endif
   if (p.To != p.Ti || p.Ho != p.Hi || p.Wo != p.Wi || p.Ti % 8) return false;
-  if ((size_t)p.N * p.Ti * p.Hi * p.Wi * p.Cin >= ((size_t)1 << 31)) return false;
+  if ((size_t)p.N * p.Ti * p.Hi * p.Wi * (p.Cin > p.Cout ? p.Cin : p.Cout) >= ((size_t)1 << 31)) return false;
   return true;
 }
 
 namespace {
-template <int CS, int TS, int EF, int PD = 2, int W = 1, int KO = 0>
+template <int CS, int TS, int EF, int PD = 2, int W = 1, int KO = 0, int HV = 1>
 hipError_t launch_tw_e(const ConvParams& p, hipStream_t s) {
   const int HW = p.Hi * p.Wi;
   const int n_cols = (HW + TW_PX - 1) / TW_PX, n_seg = p.Ti / TS;
   const long waves = (long)p.N * n_cols * n_seg;
   const size_t lds = 64 * tw_pitch(16 * CS) + 64 * 4 + 4 * 32 * TW_SP;
-  hipLaunchKernelGGL((conv_twalk_bf16<CS, TS, EF, PD, W, KO>), dim3((unsigned)((waves + 3) / 4)), dim3(256), lds, s, p,
-                     n_cols, n_seg);
+  const long blocks = (waves + 3) / 4;  // per half; HV = 2: 16 blocks per 8 block pairs
+  hipLaunchKernelGGL((conv_twalk_bf16<CS, TS, EF, PD, W, KO, HV>), dim3((unsigned)(HV == 2 ? (blocks + 7) / 8 * 16 : blocks)),
+                     dim3(256), lds, s, p, n_cols, n_seg);
   return hipGetLastError();
 }
-template <int CS, int TS>
+template <int CS, int TS, int HV>
 hipError_t launch_tw_t(const ConvParams& p, hipStream_t s) {
   switch ((p.res ? 1 : 0) | (p.relu ? 2 : 0)) {
-    case 0: return launch_tw_e<CS, TS, 0>(p, s);
-    case 1: return launch_tw_e<CS, TS, 1>(p, s);
-    case 2: return launch_tw_e<CS, TS, 2>(p, s);
-    default: return launch_tw_e<CS, TS, 3>(p, s);
+    case 0: return launch_tw_e<CS, TS, 0, 2, 1, 0, HV>(p, s);
+    case 1: return launch_tw_e<CS, TS, 1, 2, 1, 0, HV>(p, s);
+    case 2: return launch_tw_e<CS, TS, 2, 2, 1, 0, HV>(p, s);
+    default: return launch_tw_e<CS, TS, 3, 2, 1, 0, HV>(p, s);
   }
 }
-template <int CS>
+template <int CS, int HV = 1>
 hipError_t launch_tw_c(const ConvParams& p, hipStream_t s) {
   // 16-frame segments where T allows (32-frame clips: 2 per clip column, 2 of 18 input frames re-read)
-  return p.Ti % 16 == 0 ? launch_tw_t<CS, 16>(p, s) : launch_tw_t<CS, 8>(p, s);
+  return p.Ti % 16 == 0 ? launch_tw_t<CS, 16, HV>(p, s) : launch_tw_t<CS, 8, HV>(p, s);
 }
 }  // namespace
 
 hipError_t launch_twalk_bf16(const ConvParams& p, hipStream_t s) {
   if (!twalk_bf16_supported(p)) return hipErrorInvalidValue;
+#ifdef CLASFV_KNOCKOUTS
+  if (p.Cout == 128) return p.Cin == 288 ? launch_tw_c<18, 2>(p, s) : launch_tw_c<16, 2>(p, s);
+#endif
   return p.Cin == 160 ? launch_tw_c<10>(p, s) : launch_tw_c<4>(p, s);
 }
 
@@ -274,8 +294,27 @@ hipError_t launch_twalk_bf16(const ConvParams& p, hipStream_t s) {
 // tools/convbench (tpp, ko 990 + v): v = 10 * PD + W, e.g. 21 = the first form (2 frames ahead, one
 // wave per SIMD); TS 16 and the residual / ReLU flags of p
 hipError_t launch_twalk_bf16_ko(const ConvParams& p, hipStream_t s, int v) {
-  if (!twalk_bf16_supported(p) || p.Ti % 16) return hipErrorInvalidValue;
+  if (!twalk_bf16_supported(p)) return hipErrorInvalidValue;
   const int ef = (p.res ? 1 : 0) | (p.relu ? 2 : 0);
+  if (p.Cout == 128) {  // layer2 (two halves): v = 1000 PD + TS, e.g. 2016 = PD 2, TS 16
+    auto g2 = [&](auto cs) -> hipError_t {
+      constexpr int CS = decltype(cs)::value;
+      auto e = [&](auto efc) -> hipError_t {
+        constexpr int EF = decltype(efc)::value;
+        switch (v) {
+          case 1016: return p.Ti % 16 ? hipErrorInvalidValue : launch_tw_e<CS, 16, EF, 1, 1, 0, 2>(p, s);
+          case 2016: return p.Ti % 16 ? hipErrorInvalidValue : launch_tw_e<CS, 16, EF, 2, 1, 0, 2>(p, s);
+          case 1008: return launch_tw_e<CS, 8, EF, 1, 1, 0, 2>(p, s);
+          case 2008: return launch_tw_e<CS, 8, EF, 2, 1, 0, 2>(p, s);
+        }
+        return hipErrorInvalidValue;
+      };
+      return ef == 3 ? e(std::integral_constant<int, 3>{}) : e(std::integral_constant<int, 2>{});
+    };
+    if (!p.relu) return hipErrorInvalidValue;
+    return p.Cin == 288 ? g2(std::integral_constant<int, 18>{}) : g2(std::integral_constant<int, 16>{});
+  }
+  if (p.Ti % 16) return hipErrorInvalidValue;
   auto go = [&](auto cs) -> hipError_t {
     constexpr int CS = decltype(cs)::value;
     auto e = [&](auto efc) -> hipError_t {

@@ -209,6 +209,7 @@ int main(int argc, char** argv) {
     } else if (winot) CK(launch_winot_ko(p, s, ko));
     else if (tpp && ko == 990) CK(launch_twalk_bf16(p, s));  // conv_twalk_bf16 (frame-walking temporal conv)
     else if (tpp && ko > 990 && ko < 1200) CK(launch_twalk_bf16_ko(p, s, ko - 990));  // its PD / W forms, knock-outs
+    else if (tpp && ko >= 2000 && ko < 3100) CK(launch_twalk_bf16_ko(p, s, ko - 1000));  // 128-channel forms: 1000 PD + TS
     else if ((spp || tpp) && ko == 901) CK(launch_patch_bf16_v1(p, s));
     else if (spp && ko >= 950 && ko < 970) {  // conv_patch32_bf16 (32x32x16 tiles); 951..955: NB forced;
       ConvParams q = p;                        // 960..965: direct-store epilogue
