@@ -67,6 +67,16 @@ __device__ inline void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(V) : "memory");
 }
 
+// An epilogue's bias / residual load through a global-address-space (1) pointer: the compiler then knows
+// it cannot alias the LDS staging rows written between the loads and issues them together -- through
+// the generic pointer every load waited for the previous staging write: 64 serialized load -> vmcnt(0)
+// round trips per wave in conv_patch_bf16's temporal epilogue.
+template <class V, class T>
+__device__ inline V gload(const T* p) {
+  typedef const V __attribute__((address_space(1))) GV;
+  return *(GV*)(const __attribute__((address_space(1))) void*)p;
+}
+
 // address (bytes) of one 16-B LDS-DMA source: uniform base + per-lane offset (the saddr form)
 __device__ inline void dma16(const char* base, unsigned off, void* lds_dst) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + off),
@@ -252,12 +262,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
       return to < p.To && hw < HW;
     }
   };
+  // the block's bias values, one (wave-uniform) branch for all of them (a branch per load serialized
+  // the epilogue's loads)
+  f32x4 bv[NT];
+  if (p.bias) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bv[j] = gload<f32x4>(p.bias + n0 + j * 16 + 4 * q);
+  } else {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   auto finish = [&](int i, int j, size_t gm) __attribute__((always_inline)) {
     const int n = n0 + j * 16 + 4 * q;
-    f32x4 v = acc[i][j];
-    if (p.bias) v += *reinterpret_cast<const f32x4*>(p.bias + n);
+    f32x4 v = acc[i][j] + bv[j];
     if constexpr (EF & 1) {
-      const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + gm * p.Cout + n);
+      const bf16x4 r = gload<bf16x4>(res + gm * p.Cout + n);
       v += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
     }
     if constexpr (EF & 2) {
@@ -636,9 +655,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
     f32x4 v = {acc[rb][cb][4 * g], acc[rb][cb][4 * g + 1], acc[rb][cb][4 * g + 2], acc[rb][cb][4 * g + 3]};
     // p.bias is required (patch32_bf16_supported): an unguarded load, so a column block's loads issue
     // together (one vmcnt wait) instead of one guarded load and wait each
-    v += *reinterpret_cast<const f32x4*>(p.bias + n);
+    v += gload<f32x4>(p.bias + n);
     if constexpr (RES) {
-      const bf16x4 rv = *reinterpret_cast<const bf16x4*>(res + gm * p.Cout + n);
+      const bf16x4 rv = gload<bf16x4>(res + gm * p.Cout + n);
       v += f32x4{(float)rv[0], (float)rv[1], (float)rv[2], (float)rv[3]};
     }
     if constexpr (RELU) {
@@ -1028,9 +1047,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   __bf16* y = reinterpret_cast<__bf16*>(p.y);
   auto finish = [&](int i, int j, size_t gm) __attribute__((always_inline)) {
     const int n = n0 + j * 16 + 4 * q;
-    f32x4 v = acc[i][j] + *reinterpret_cast<const f32x4*>(p.bias + n);
+    f32x4 v = acc[i][j] + gload<f32x4>(p.bias + n);
     if constexpr (EF & 1) {
-      const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + gm * p.Cout + n);
+      const bf16x4 r = gload<bf16x4>(res + gm * p.Cout + n);
       v += f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
     }
     if constexpr (EF & 2) {
