@@ -94,7 +94,11 @@ struct DecParams {
   int N, T, H, W;
   int bf16;           // comb_2 on bf16 MFMAs (bf16 engines; taps, heads and outputs stay fp32)
   int x3;             // fp32 engines: comb_2 as six bf16 products of 3-way split operands (fp32-accurate)
+  void* idx;          // device scratch of decoder_index_bytes(T, H, W): the per-launch source-index table
+                      // (launch_decoder fills it on the stream before the decoder reads it)
 };
+// bytes of DecParams::idx: per tap, T frame + H row + W column entries of 16 B
+inline size_t decoder_index_bytes(int T, int H, int W) { return (size_t)4 * (T + H + W) * 16; }
 
 // Launchers (stream-ordered, no synchronisation). Return hipError_t of the launch.
 hipError_t launch_conv(const ConvParams& p, int mt, int bn, hipStream_t s);

@@ -60,7 +60,7 @@ struct DecGeo {
 static_assert(DecGeo<8>::STAGE_FLOATS == 105 * PIX && DecGeo<8>::kLoadsTotal == 12, "8-row tile geometry");
 
 struct Win {
-  int t0, t1, nf, r0, nr, c0, nc;
+  int t0, t1, r0, nr, c0, nc;
   float lt0, lt1;
 };
 
@@ -70,6 +70,41 @@ __device__ inline void src_index(float s, int dst, int in, int& i0, int& i1, flo
   l1 = fminf(fmaxf(f - (float)i0, 0.f), 1.f);
   i1 = i0 + (i0 < in - 1 ? 1 : 0);
   l0 = 1.f - l1;
+}
+
+// The source-index table of one launch (DecParams::idx): per tap i at entry i (T + H + W), the T
+// output frames' (t0, t1, lt0, lt1) -- the temporal blend the staging applies, already collapsed to
+// one frame (t1 = t0, weights 1 and 0) where the decoder reads one (tap 0, or a zero second weight)
+// -- then the H output rows' and the W output columns' src_index (i0, i1, l0, l1). The same device
+// src_index over the same scales as the decoder's own evaluation, so the decoder reads back the
+// values it used to compute per wave: ≈ 240 VALU of index arithmetic (floors, clamps, conversions)
+// and ≈ 60 readfirstlanes per wave become a few scalar loads and one vector load per tap.
+struct DecIdx {
+  int i0, i1;
+  float l0, l1;
+};
+
+__global__ __launch_bounds__(256) void decoder_index_kernel(DecParams p) {
+  const int per = p.T + p.H + p.W;
+  DecIdx* tab = reinterpret_cast<DecIdx*>(p.idx);
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < 4 * per; e += gridDim.x * 256) {
+    const int i = e / per, k = e - i * per;
+    const DecTap& tp = p.tap[i];
+    DecIdx d;
+    if (k < p.T) {
+      float la, lb;
+      src_index(tp.st, k, tp.T, d.i0, d.i1, la, lb);
+      const bool two = lb > 0.f && d.i1 != d.i0 && i > 0;  // decoder_kernel: DecGeo::kFrames[i] == 2
+      d.i1 = two ? d.i1 : d.i0;
+      d.l0 = two ? la : 1.f;
+      d.l1 = two ? lb : 0.f;
+    } else if (k < p.T + p.H) {
+      src_index(tp.sh, k - p.T, tp.H, d.i0, d.i1, d.l0, d.l1);
+    } else {
+      src_index(tp.sw, k - p.T - p.H, tp.W, d.i0, d.i1, d.l0, d.l1);
+    }
+    tab[e] = d;
+  }
 }
 
 // tanh(x) = 1 - 2 / (e^(2x) + 1) on v_exp_f32 and v_rcp_f32: a few VALU instructions instead of
@@ -145,7 +180,11 @@ __device__ inline void split3_bf16x8(f32x4 a, f32x4 b, bf16x8& hi, bf16x8& mid, 
 // accumulation -- fp32-accurate, on the bf16 matrix rate (12 instead of 32 MFMA slots; on gfx950 the
 // f32 MFMA shares the f32 vector rate with the interpolation, which the bf16 MFMA does not). W2's
 // pieces come split on the host (DecParams::w2x3), h1's are split here.
-template <bool X3, bool HX3>
+// W2S (bf16 engines, the knock-out builds' legacy form): W2's hi / lo pieces split here from the fp32
+// W2 in every wave; otherwise read from DecParams::w2x3, whose mid piece is exactly that lo (the
+// bf16 of the remainder w - hi, exact in fp32, rounded to nearest either way): bit-identical, 64 split
+// values per lane fewer
+template <bool X3, bool HX3, bool W2S = false>
 __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[2][4], int t, int n, int h0, int w0,
                                           int wid, int q, int l16) {
   bf16x8 hh[2][2], hl[2][2], hm[2][2];
@@ -161,15 +200,18 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
   f32x4 acc[2][4];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
-    const float* wr = p.w2 + (16 * nt + l16) * 64 + 4 * q;
+    [[maybe_unused]] const float* wr = p.w2 + (16 * nt + l16) * 64 + 4 * q;
     bf16x8 wh_[2], wl_[2], wm_[2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
+      const bf16x8* w3 = reinterpret_cast<const bf16x8*>(p.w2x3) + ((nt * 2 + kb) * 16 + l16) * 4 + q;
       if constexpr (X3) {
-        const bf16x8* w3 = reinterpret_cast<const bf16x8*>(p.w2x3) + ((nt * 2 + kb) * 16 + l16) * 4 + q;
         wh_[kb] = w3[0];
         wm_[kb] = w3[512];
         wl_[kb] = w3[1024];
+      } else if constexpr (!W2S) {
+        wh_[kb] = w3[0];
+        wl_[kb] = w3[512];
       } else {
         split_bf16x8(*reinterpret_cast<const f32x4*>(wr + 32 * kb), *reinterpret_cast<const f32x4*>(wr + 32 * kb + 16),
                      wh_[kb], wl_[kb]);
@@ -271,10 +313,15 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
 // TROWS: tile rows (8: 4 waves per block; 16: 8 waves, half the blocks and less halo per voxel)
 // MODE + 8 (SC): the staging blend and the interpolation as single-lane v_fma_f32 / v_mul_f32
 // (the same operations and order as the packed form, so bit-identical)
+// MODE_ + 16 (LIX, knock-out builds): every wave evaluates its source indices itself (src_index per
+// tap and voxel row / column, the staging windows) instead of reading DecParams::idx; + 32 (bf16
+// engines): W2's pieces split in the kernel (decoder_heads_bf16's W2S). Both bit-identical.
 template <int MODE_, int TROWS = 8>
 __global__ __launch_bounds__(32 * TROWS) __attribute__((amdgpu_waves_per_eu((MODE_ & 7) == 4 ? 4 : 5, (MODE_ & 7) == 4 ? 4 : 5))) void decoder_kernel(DecParams p) {
   constexpr int MODE = MODE_ & 7;
   constexpr bool SC = (MODE_ & 8) != 0;
+  constexpr bool LIX = (MODE_ & 16) != 0;
+  constexpr bool W2S = (MODE_ & 32) != 0;
   using G = DecGeo<TROWS>;
   constexpr int TILE_H = TROWS, NTHR = G::NTHR;
   constexpr int BF = MODE == 1 || MODE == 4;
@@ -295,29 +342,46 @@ __global__ __launch_bounds__(32 * TROWS) __attribute__((amdgpu_waves_per_eu((MOD
   const int h0 = (tile / tiles_w) * TILE_H, w0 = (tile % tiles_w) * TILE_W;
 
 
-  // Source windows of the four taps.
+  // Source windows of the four taps: the tile's rows h0 .. h0 + TILE_H - 1 read source rows
+  // i0(h0) .. i1(h0 + TILE_H - 1) (i1 = min(floor + 1, in - 1), the window's last row), columns the same
+  const DecIdx* tab = reinterpret_cast<const DecIdx*>(p.idx);
+  const int per = p.T + p.H + p.W;
   Win win[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const DecTap& tp = p.tap[i];
     Win w;
-    int a, b;
-    float la, lb;
-    src_index(tp.st, t, tp.T, a, b, la, lb);
-    const bool two = lb > 0.f && b != a && G::kFrames[i] == 2;  // else the blend below is exactly P[t0]
-    w.t0 = uni(a);
-    w.t1 = uni(two ? b : a);
-    w.lt0 = unif(two ? la : 1.f);
-    w.lt1 = unif(two ? lb : 0.f);
-    w.nf = two ? 2 : 1;
-    const int r0 = min((int)floorf(tp.sh * (float)h0), tp.H - 1);
-    const int r1 = min((int)floorf(tp.sh * (float)(h0 + TILE_H - 1)) + 1, tp.H - 1);
-    const int c0 = min((int)floorf(tp.sw * (float)w0), tp.W - 1);
-    const int c1 = min((int)floorf(tp.sw * (float)(w0 + TILE_W - 1)) + 1, tp.W - 1);
-    w.r0 = uni(r0);
-    w.nr = uni(min(r1 - r0 + 1, G::kMaxRows[i]));
-    w.c0 = uni(c0);
-    w.nc = uni(min(c1 - c0 + 1, G::kMaxCols[i]));
+    if constexpr (LIX) {
+      int a, b;
+      float la, lb;
+      src_index(tp.st, t, tp.T, a, b, la, lb);
+      const bool two = lb > 0.f && b != a && G::kFrames[i] == 2;  // else the blend below is exactly P[t0]
+      w.t0 = uni(a);
+      w.t1 = uni(two ? b : a);
+      w.lt0 = unif(two ? la : 1.f);
+      w.lt1 = unif(two ? lb : 0.f);
+      const int r0 = min((int)floorf(tp.sh * (float)h0), tp.H - 1);
+      const int r1 = min((int)floorf(tp.sh * (float)(h0 + TILE_H - 1)) + 1, tp.H - 1);
+      const int c0 = min((int)floorf(tp.sw * (float)w0), tp.W - 1);
+      const int c1 = min((int)floorf(tp.sw * (float)(w0 + TILE_W - 1)) + 1, tp.W - 1);
+      w.r0 = uni(r0);
+      w.nr = uni(min(r1 - r0 + 1, G::kMaxRows[i]));
+      w.c0 = uni(c0);
+      w.nc = uni(min(c1 - c0 + 1, G::kMaxCols[i]));
+    } else {
+      const DecIdx* ti = tab + i * per;
+      const DecIdx ft = ti[t];  // block-uniform: scalar loads
+      w.t0 = ft.i0;
+      w.t1 = ft.i1;
+      w.lt0 = ft.l0;
+      w.lt1 = ft.l1;
+      const int r0 = ti[p.T + h0].i0, r1 = ti[p.T + h0 + TILE_H - 1].i1;
+      const int c0 = ti[per - p.W + w0].i0, c1 = ti[per - p.W + w0 + TILE_W - 1].i1;
+      w.r0 = r0;
+      w.nr = min(r1 - r0 + 1, G::kMaxRows[i]);
+      w.c0 = c0;
+      w.nc = min(c1 - c0 + 1, G::kMaxCols[i]);
+    }
     win[i] = w;
   }
   // All staging loads are issued before the first LDS write (fixed per-tap trip counts, predicated),
@@ -400,11 +464,20 @@ __global__ __launch_bounds__(32 * TROWS) __attribute__((amdgpu_waves_per_eu((MOD
     const Win& w = win[i];
     int x0, x1, ya0, ya1, yb0, yb1;
     float lx0, lx1, la0, la1, lb0, lb1;
-    src_index(tp.sw, w0 + l16, tp.W, x0, x1, lx0, lx1);
-    src_index(tp.sh, hr, tp.H, ya0, ya1, la0, la1);
-    src_index(tp.sh, hr + 1, tp.H, yb0, yb1, lb0, lb1);
-    ya0 = uni(ya0), ya1 = uni(ya1), yb0 = uni(yb0), yb1 = uni(yb1);
-    la0 = unif(la0), la1 = unif(la1), lb0 = unif(lb0), lb1 = unif(lb1);
+    if constexpr (LIX) {
+      src_index(tp.sw, w0 + l16, tp.W, x0, x1, lx0, lx1);
+      src_index(tp.sh, hr, tp.H, ya0, ya1, la0, la1);
+      src_index(tp.sh, hr + 1, tp.H, yb0, yb1, lb0, lb1);
+      ya0 = uni(ya0), ya1 = uni(ya1), yb0 = uni(yb0), yb1 = uni(yb1);
+      la0 = unif(la0), la1 = unif(la1), lb0 = unif(lb0), lb1 = unif(lb1);
+    } else {
+      const DecIdx* ti = tab + i * per;
+      const DecIdx cx = ti[per - p.W + w0 + l16];  // one 16-B load per lane
+      const DecIdx ra = ti[p.T + hr], rb = ti[p.T + hr + 1];  // wave-uniform: scalar loads
+      x0 = cx.i0, x1 = cx.i1, lx0 = cx.l0, lx1 = cx.l1;
+      ya0 = ra.i0, ya1 = ra.i1, la0 = ra.l0, la1 = ra.l1;
+      yb0 = rb.i0, yb1 = rb.i1, lb0 = rb.l0, lb1 = rb.l1;
+    }
     const int nrows = yb1 - ya0 + 1;  // 1..3, wave-uniform
     const float* fb = stage + G::kPixOff[i] * PIX + 4 * q + (ya0 - w.r0) * G::kMaxCols[i] * PIX;
     const float* c0p = fb + (x0 - w.c0) * PIX;
@@ -466,7 +539,7 @@ __global__ __launch_bounds__(32 * TROWS) __attribute__((amdgpu_waves_per_eu((MOD
       for (int j = 0; j < 4; ++j) h1[mt][c][j] = relu1(h1[mt][c][j]);
 
   if constexpr (BF) {
-    decoder_heads_bf16<MODE == 4, true>(p, h1, t, n, h0, w0, wid, q, l16);
+    decoder_heads_bf16<MODE == 4, true, W2S>(p, h1, t, n, h0, w0, wid, q, l16);
     return;
   }
   // 3. h2^T[n][v] = sum_k W2[n][k] h1[v][k]; MFMA j of lane group q covers k = 16c + 4q + j
@@ -564,16 +637,26 @@ static hipError_t launch_dec(const DecParams& p, hipStream_t s, int mode, int th
   static_assert(DecGeo<16>::STAGE_FLOATS * 4 <= 64 * 1024, "default dynamic LDS limit");
   const size_t lds = (size_t)(th == 16 ? DecGeo<16>::STAGE_FLOATS : DecGeo<8>::STAGE_FLOATS) * 4;
   void (*k)(DecParams) = nullptr;
-  if (th == 16)
-    k = mode == 1 ? decoder_kernel<1, 16> : mode == 4 ? decoder_kernel<4, 16> : decoder_kernel<0, 16>;
-  else
-    k = mode == 1 ? decoder_kernel<1> : mode == 4 ? decoder_kernel<4> : decoder_kernel<0>;
+  if (th == 8) k = mode == 1 ? decoder_kernel<1> : mode == 4 ? decoder_kernel<4> : mode == 0 ? decoder_kernel<0> : nullptr;
 #ifdef CLASFV_KNOCKOUTS
+  if (th == 16 && mode < 16) k = mode == 1 ? decoder_kernel<1, 16> : mode == 4 ? decoder_kernel<4, 16> : decoder_kernel<0, 16>;
   if (mode == 2) k = th == 16 ? decoder_kernel<2, 16> : decoder_kernel<2>;
   if (mode == 3) k = th == 16 ? decoder_kernel<3, 16> : decoder_kernel<3>;
   if (mode == 12) k = th == 16 ? decoder_kernel<12, 16> : decoder_kernel<12>;
   if (mode == 9) k = th == 16 ? decoder_kernel<9, 16> : decoder_kernel<9>;
+  // the round-6 forms before the index table and the host-split bf16 W2 pieces
+  if (th == 8 && mode == 1 + 16 + 32) k = decoder_kernel<1 + 16 + 32>;
+  if (th == 8 && mode == 4 + 16) k = decoder_kernel<4 + 16>;
+  if (th == 8 && mode == 0 + 16) k = decoder_kernel<0 + 16>;
+  if (th == 8 && mode == 1 + 16) k = decoder_kernel<1 + 16>;
+  if (th == 8 && mode == 1 + 32) k = decoder_kernel<1 + 32>;
 #endif
+  if (!k) return hipErrorInvalidValue;
+  if (!(mode & 16)) {  // the source-index table this launch reads, filled on the same stream first
+    if (!p.idx) return hipErrorInvalidValue;
+    const int ne = 4 * (p.T + p.H + p.W);
+    hipLaunchKernelGGL(decoder_index_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, s, p);
+  }
   hipLaunchKernelGGL(k, dim3((unsigned)nb), dim3(32 * th), lds, s, p);
   return hipGetLastError();
 }
@@ -623,10 +706,15 @@ hipError_t launch_decoder(const DecParams& p, hipStream_t s) {
 }
 
 #ifdef CLASFV_KNOCKOUTS
-// tools/convbench.hip: ko 0 = 8-row tiles; 2, 3 = decoder_kernel's knock-out modes; + 16: 16-row tiles
+// tools/convbench.hip: ko 0 = 8-row tiles; 2, 3 = decoder_kernel's knock-out modes; + 16: 16-row tiles;
+// + 32: single-lane interpolation FMAs; + 64: per-wave index arithmetic (no table); + 128: bf16 W2
+// split in the kernel
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko) {
   const int m = ko & 15;
   const int base = m == 2 || m == 3 ? m : (p.bf16 ? 1 : p.x3 ? 4 : 0);
-  return launch_dec(p, s, (ko & 32) && (base == 1 || base == 4) ? base + 8 : base, (ko & 16) ? 16 : 8);
+  int mode = (ko & 32) && (base == 1 || base == 4) ? base + 8 : base;
+  if (ko & 64) mode += 16;
+  if ((ko & 128) && base == 1) mode += 32;
+  return launch_dec(p, s, mode, (ko & 16) ? 16 : 8);
 }
 #endif

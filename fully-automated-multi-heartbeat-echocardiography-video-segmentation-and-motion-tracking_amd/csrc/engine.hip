@@ -568,7 +568,7 @@ struct Layout {
   size_t off[32];
   size_t total;
 };
-enum Buf { XIN, S0, X0, MID, TA, DSB, L1A, L1, L2A, L2, L3A, L3, L4A, L4, P01, PP2, PP3, PP4, NBUF };
+enum Buf { XIN, S0, X0, MID, TA, DSB, L1A, L1, L2A, L2, L3A, L3, L4A, L4, P01, PP2, PP3, PP4, DIDX, NBUF };
 
 void make_layout(int N, int T, int H, int W, Layout& L) {
   const size_t T1 = T, H2 = H / 2, W2 = W / 2;
@@ -595,6 +595,7 @@ void make_layout(int N, int T, int H, int W, Layout& L) {
   sz[PP2] = (size_t)N * (T / 2) * (H / 4) * (W / 4) * 64;
   sz[PP3] = (size_t)N * (T / 4) * (H / 8) * (W / 8) * 64;
   sz[PP4] = (size_t)N * (T / 8) * (H / 16) * (W / 16) * 64;
+  sz[DIDX] = decoder_index_bytes(T, H, W) / sizeof(float);  // the decoder's source-index table
   size_t o = 0;
   for (int i = 0; i < NBUF; ++i) {
     L.off[i] = o;
@@ -1081,6 +1082,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   d.bf16 = h->dtype == CLASFV_DTYPE_BF16 && !(h->tune.vflags & CLASFV_VARIANT_NO_DECODER_BF16);
   d.w2x3 = h->w2x3;
   d.x3 = h->dtype != CLASFV_DTYPE_BF16 && !(h->tune.vflags & CLASFV_VARIANT_NO_DECODER_X3);
+  d.idx = buf(DIDX);
   HIP_TRY(launch_decoder(d, s));
   // comb_2 (64x64) and the heads (6 useful of the 16 rows of their MFMA tile) per output voxel, in the
   // products of the pipe they run on: fp32 engines six split-bf16 products each (bf16 pipe), bf16

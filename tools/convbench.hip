@@ -404,6 +404,7 @@ static int run_decoder(int N, int T, int H, int W, int iters, const std::vector<
   CK(hipMalloc((void**)&d.seg, (size_t)N * 2 * T * H * W * 4));
   CK(hipMalloc((void**)&d.mot, (size_t)N * 4 * T * H * W * 4));
   d.N = N, d.T = T, d.H = H, d.W = W;
+  CK(hipMalloc(&d.idx, decoder_index_bytes(T, H, W)));
   d.bf16 = getenv("CB_BF16") ? 1 : 0;
   if (getenv("CB_X3") || d.bf16) {  // split-bf16 comb_2 (X3) and heads: W2 / Wh pieces in lane order
     std::vector<float> w2(64 * 64), wh(8 * 64);
