@@ -63,6 +63,8 @@ def parse(argv=None):
     ap.add_argument("--step", type=int, default=1)
     ap.add_argument("--fuse-method", default="simple")
     ap.add_argument("--batch-size", type=int, default=32, help="clips per forward call")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="c1: consecutive steps issued round-robin on this many HIP streams (videos in flight)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--parity-random", type=int, default=1,
                     help="also check the same workload with the random and deep weight recipes against their CPU "
@@ -132,14 +134,17 @@ def host_cpus():
     return max(1, n)
 
 
-def timed(fn, steps, warmup, engine, world, dev):
-    """Run fn warmup times, then time exactly `steps` calls bracketed by barrier + synchronize, with
-    the engine's per-kernel HIP events on. Returns (max-over-ranks seconds, kernel timing, last)."""
+def timed(fn, steps, warmup, engine, world, dev, kt_fn=None):
+    """Run fn warmup times, then time exactly `steps` calls bracketed by barrier + synchronize (the
+    throughput pass, no per-launch events). Then a kernel-timing pass: `steps` more calls of kt_fn
+    (default fn) with the engine's per-kernel HIP events on. kt_fn is the one-stream form of a step
+    whose throughput pass keeps several steps in flight on different streams: there an event interval
+    would also hold the other streams' kernels, so per-launch durations come from the serial pass.
+    Returns (max-over-ranks seconds of the throughput pass, kernel timing, last result)."""
     out = None
     for _ in range(warmup):
         out = fn()
     torch.cuda.synchronize()
-    engine.set_kernel_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -150,11 +155,15 @@ def timed(fn, steps, warmup, engine, world, dev):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    kt = engine.kernel_timing()
-    engine.set_kernel_timing(False)
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    engine.set_kernel_timing(True)
+    for _ in range(steps):
+        (kt_fn or fn)()
+    torch.cuda.synchronize()
+    kt = engine.kernel_timing()
+    engine.set_kernel_timing(False)
     return float(t.item()), kt, out
 
 
@@ -586,12 +595,27 @@ def run_c1(args, model, world, rank, dev):
     plans, n_total = D.global_clip_plan(lengths, args.fuse, args.step)
     lo, hi = D.shard_bounds(n_total, rank, world)
 
-    def step():
+    # steps in flight: consecutive steps round-robin on `inflight` streams, so step k + 1's stem / layer1
+    # grids overlap step k's small-grid tail (layer3 / layer4, decoder, fusion); the engine keeps one
+    # workspace per stream. Only where no step moves data between ranks (the c1 layout: one video per
+    # rank), so every rank's collectives stay in one order.
+    inflight = max(1, args.inflight) if world == 1 or D.rows_exchanged(D.owner_of_clips(plans, world), world) == 0 else 1
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(inflight - 1)]
+    issued = [0]
+    torch.cuda.synchronize()  # the videos exist before any stream reads them
+
+    def serial_step():
         return D.segment_videos_sharded(videos, model, num_clips=args.fuse, step=args.step,
                                         fuse_method=args.fuse_method, rank=rank, world=world,
                                         batch_size=args.batch_size, lengths=lengths)
 
-    dt, ktimes, out = timed(step, args.steps, args.warmup, eng, world, dev)
+    def step():
+        s = streams[issued[0] % len(streams)]
+        issued[0] += 1
+        with torch.cuda.stream(s):
+            return serial_step()
+
+    dt, ktimes, out = timed(step, args.steps, args.warmup, eng, world, dev, kt_fn=serial_step)
     value = n_total * args.steps / dt
     peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else FP32_PEAK_TFLOPS
     fwd = forward_stats(ktimes, (hi - lo) * args.steps, GFLOP_PER_CLIP, peak, args.dtype)
@@ -605,7 +629,7 @@ def run_c1(args, model, world, rank, dev):
     if args.extra_bf16 and args.dtype == "fp32":
         ref_masks = {k: v.clone() for k, v in out.items()}
         model.set_compute_dtype("bf16")
-        dt16, k16, out16 = timed(step, args.steps, args.warmup, eng, world, dev)
+        dt16, k16, out16 = timed(step, args.steps, args.warmup, eng, world, dev, kt_fn=serial_step)
         from clasfv_amd.echo import categorical_dice
         d16 = [1.0 - categorical_dice(out16[k].cpu().numpy(), ref_masks[k].cpu().numpy(), 1) for k in out16]
         bf16 = {"value": round(n_total * args.steps / dt16, 3), "unit": "clips/s",
@@ -681,6 +705,11 @@ def run_c1(args, model, world, rank, dev):
                                "(30 x 32-frame clips) + per-frame SIMPLE label fusion",
                    "videos_per_gpu": args.videos_per_gpu, "frames": args.frames, "fuse": args.fuse,
                    "step": args.step, "clips_per_step": n_total, "batch_size": args.batch_size,
+                   "steps_in_flight": inflight,
+                   "timing": "value / ms_per_step: the throughput pass, consecutive steps round-robin on "
+                             "steps_in_flight HIP streams (one engine workspace per stream), no per-launch "
+                             "events; roofline / forward / kernels: a second pass of the same steps on one "
+                             "stream with the engine's per-launch HIP events",
                    "parallelism": f"clip-shard x{world}; videos fused on the rank holding their clips "
                                   f"(owner all_to_all of logit margins only for straddling videos)"},
         "roofline": kernel_roofline(ktimes, peak, args.dtype),

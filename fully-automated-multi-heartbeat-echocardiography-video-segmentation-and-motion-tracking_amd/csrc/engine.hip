@@ -193,15 +193,24 @@ struct clasfv_engine {
   bool ready = false;
   int dtype = CLASFV_DTYPE_FP32;  // compute dtype of the encoder convs
   Tuning tune;                    // kernel variants / tile overrides (environment at create)
-  // workspace arena
-  char* arena = nullptr;
-  size_t arena_bytes = 0;
   float* zero = nullptr;  // 256 zero bytes for padding taps
-  // side stream of clasfv_forward: the decoder projections of the stem/layer1, layer2 and layer3 taps
-  // run there as soon as their tap exists, filling the CUs the backbone's later (small-grid) convs
-  // leave idle; the decoder waits for them (events, no host synchronisation)
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // One forward context per launch stream: the workspace arena (activations, mid tensors, decoder taps
+  // and index table) and the side stream with its fork / join events. The decoder projections of the
+  // stem/layer1, layer2 and layer3 taps run on the side stream as soon as their tap exists, filling the
+  // CUs the backbone's later (small-grid) convs leave idle; the decoder waits for them (events, no host
+  // synchronisation). Forwards issued on different streams own different contexts, so they may run
+  // concurrently on one handle (a serving pipeline with two videos in flight): each one's arena is
+  // touched only by work ordered on its own stream. Forwards on one stream reuse its context in order.
+  struct Ctx {
+    hipStream_t stream = nullptr;  // the launch stream this context belongs to
+    char* arena = nullptr;
+    size_t arena_bytes = 0;
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    uint64_t last_use = 0;
+  };
+  std::vector<Ctx*> ctxs;
+  uint64_t ctx_clock = 0;
   // per-kernel HIP-event timing of clasfv_forward (clasfv_set_kernel_timing)
   bool ktime = false;
   std::vector<hipEvent_t> evs;  // event pool; evs[0..nev) recorded since the last read
@@ -680,16 +689,19 @@ int clasfv_destroy(clasfv_t h) {
     (void)hipFree(c.dw);
     (void)hipFree(c.dx3);
   }
-  if (h->side) (void)hipStreamDestroy(h->side);
-  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  for (auto* c : h->ctxs) {
+    if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    (void)hipFree(c->arena);
+    delete c;
+  }
   (void)hipFree(h->b1);
   (void)hipFree(h->w2);
   (void)hipFree(h->w2x3);
   (void)hipFree(h->b2);
   (void)hipFree(h->wh);
   (void)hipFree(h->bh);
-  (void)hipFree(h->arena);
   (void)hipFree(h->zero);
   for (auto e : h->evs) (void)hipEventDestroy(e);
   delete h;
@@ -897,7 +909,12 @@ int clasfv_finalize(clasfv_t h) {
   return CLASFV_OK;
 }
 
-int64_t clasfv_workspace_bytes(clasfv_t h) { return h ? (int64_t)h->arena_bytes : 0; }
+int64_t clasfv_workspace_bytes(clasfv_t h) {
+  if (!h) return 0;
+  int64_t b = 0;
+  for (auto* c : h->ctxs) b += (int64_t)c->arena_bytes;
+  return b;
+}
 
 int clasfv_set_compute_dtype(clasfv_t h, int dtype) {
   if (!h) return fail(CLASFV_EINVAL, "null handle");
@@ -932,16 +949,36 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   DEVICE_GUARD(h->device);
   Layout L;
   make_layout(N, T, H, W, L);
-  if (L.total > h->arena_bytes) {
-    // The arena may still be in use by work queued earlier on any stream.
-    HIP_TRY(hipDeviceSynchronize());
-    (void)hipFree(h->arena);
-    h->arena = nullptr;
-    h->arena_bytes = 0;
-    HIP_TRY(hipMalloc(&h->arena, L.total));
-    h->arena_bytes = L.total;
+  // this stream's context: created on first use; past kMaxCtx streams the least recently used one is
+  // taken over once the device is idle (no queued work can still be using its arena)
+  clasfv_engine::Ctx* cx = nullptr;
+  for (auto* c : h->ctxs)
+    if (c->stream == s) cx = c;
+  if (!cx) {
+    constexpr size_t kMaxCtx = 4;
+    if (h->ctxs.size() < kMaxCtx) {
+      cx = new clasfv_engine::Ctx();
+      h->ctxs.push_back(cx);
+    } else {
+      HIP_TRY(hipDeviceSynchronize());
+      cx = h->ctxs.front();
+      for (auto* c : h->ctxs)
+        if (c->last_use < cx->last_use) cx = c;
+    }
+    cx->stream = s;
   }
-  auto buf = [&](int b) { return reinterpret_cast<void*>(h->arena + L.off[b]); };
+  cx->last_use = ++h->ctx_clock;
+  if (L.total > cx->arena_bytes) {
+    // The arena may still be in use by work queued earlier on its stream.
+    HIP_TRY(hipDeviceSynchronize());
+    (void)hipFree(cx->arena);
+    cx->arena = nullptr;
+    cx->arena_bytes = 0;
+    HIP_TRY(hipMalloc(&cx->arena, L.total));
+    cx->arena_bytes = L.total;
+  }
+  char* const arena = cx->arena;
+  auto buf = [&](int b) { return reinterpret_cast<void*>(arena + L.off[b]); };
   int last_ev = h->ktime ? tick(h, s) : -1;
   auto timed = [&](const char* name, double gflop, double xgflop) {
     if (last_ev < 0) return;
@@ -951,38 +988,38 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
   };
   // scratch for a temporal conv reading MID: the rest of MID past its input
   const size_t mid_bytes = L.off[MID + 1] - L.off[MID];
-  if (!h->side) {
-    HIP_TRY(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+  if (!cx->side) {
+    HIP_TRY(hipStreamCreateWithFlags(&cx->side, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&cx->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&cx->ev_join, hipEventDisableTiming));
   }
   // Once work is forked to the side stream, every exit of this call (the error returns included)
   // leaves s ordered after everything queued there, so the caller's next use of the arena or the
   // outputs cannot race the projections.
   struct SideJoin {
-    clasfv_engine* h;
+    clasfv_engine::Ctx* cx;
     hipStream_t s;
     bool pending = false;
     hipError_t join() {
       if (!pending) return hipSuccess;
       pending = false;
-      hipError_t e = hipEventRecord(h->ev_join, h->side);
-      return e != hipSuccess ? e : hipStreamWaitEvent(s, h->ev_join, 0);
+      hipError_t e = hipEventRecord(cx->ev_join, cx->side);
+      return e != hipSuccess ? e : hipStreamWaitEvent(s, cx->ev_join, 0);
     }
     ~SideJoin() { (void)join(); }
-  } side_join{h, s};
+  } side_join{cx, s};
   // a decoder projection on the side stream once its tap is complete on s (timed with its own events;
   // with kernel timing on, the layer4 launches on s run concurrently with these, so their event
   // intervals overlap: the per-kernel sums of a forward exceed its wall time by about the overlap)
   auto run_side = [&](const Conv& c, const void* xin, const Shape5& in, void* y, Shape5& out, const void* x2) {
-    HIP_TRY(hipEventRecord(h->ev_fork, s));
-    HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    HIP_TRY(hipEventRecord(cx->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(cx->side, cx->ev_fork, 0));
     side_join.pending = true;
-    const int e0 = h->ktime ? tick(h, h->side) : -1;
+    const int e0 = h->ktime ? tick(h, cx->side) : -1;
     const char* kname = "";
-    int rc_ = run_conv(c, xin, in, y, out, nullptr, false, h->side, h->zero, x2, &kname, h->tune);
+    int rc_ = run_conv(c, xin, in, y, out, nullptr, false, cx->side, h->zero, x2, &kname, h->tune);
     if (!rc_ && e0 >= 0) {
-      const int e1 = tick(h, h->side);
+      const int e1 = tick(h, cx->side);
       if (e1 >= 0) h->recs.push_back({kname, conv_gflop(c, out), conv_exec_gflop(c, out, kname), e0, e1});
     }
     return rc_;
@@ -995,7 +1032,7 @@ int clasfv_forward(clasfv_t h, const float* x, int N, int T, int H, int W, float
     if (xin == buf(MID)) {
       const size_t used = ((size_t)in.n * in.t * in.h * in.w * in.c * sizeof(float) + 255) / 256 * 256;
       if (used < mid_bytes) {
-        scratch = h->arena + L.off[MID] + used;
+        scratch = arena + L.off[MID] + used;
         scratch_bytes = mid_bytes - used;
       }
     }

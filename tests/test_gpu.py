@@ -133,6 +133,51 @@ def test_forward_batch_is_per_clip_exact_winot_nt_switch(model):
         assert torch.equal(s1[0], seg[i]) and torch.equal(m1[0], mot[i]), i
 
 
+def test_forwards_on_concurrent_streams_equal_serial(model):
+    """One engine handle keeps a workspace per launch stream (csrc/engine.hip Ctx), so forwards issued
+    on different streams without a host sync in between -- two or more videos in flight, bench.py
+    --inflight -- run concurrently and each equals the serial result bit for bit; past four streams
+    the least recently used workspace is taken over after a device sync."""
+    rng = np.random.default_rng(91)
+    xs = [torch.from_numpy(rng.uniform(0, 1, (2, 3, 32, 64, 64)).astype(np.float32)).cuda() for _ in range(6)]
+    ref = [model(x) for x in xs]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(6)]
+    for rnd in range(2):  # round 2 reuses round 1's streams (their contexts; six streams > four contexts)
+        got = []
+        for x, s in zip(xs, streams):
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                got.append(model(x))
+        torch.cuda.synchronize()
+        for i, ((s0, m0), (s1, m1)) in enumerate(zip(ref, got)):
+            assert torch.equal(s0, s1) and torch.equal(m0, m1), (rnd, i)
+
+
+def test_segment_videos_two_streams_in_flight(echo_model):
+    """bench.py --inflight 2: consecutive fusion steps of one device video on two streams give the
+    serial step's masks."""
+    from clasfv_amd import dist as D
+    import clasfv_amd.synthetic as S
+    v = torch.as_tensor(S.echo_video(120, seed=3)).cuda()
+
+    def step():
+        return D.segment_videos_sharded([v], echo_model, num_clips=5, step=1, fuse_method="simple")[0]
+
+    ref = step()
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for k in range(4):
+        s = streams[k % 2]
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            outs.append(step())
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, ref)
+
+
 @pytest.mark.parametrize("shape", [(2, 3, 32, 112, 112), (3, 3, 24, 80, 112)])
 def test_bf16_forward_batch_is_per_clip_exact(shape):
     """config[4] engines: every kernel choice is a per-clip shape rule too (conv_patch32_bf16 is taken
