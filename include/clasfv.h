@@ -108,10 +108,15 @@ int clasfv_param_info(clasfv_t h, int i, const char** name, int* ndim, int64_t d
 int clasfv_load_param(clasfv_t h, const char* name, const float* host_data, int64_t numel);
 /* Fold eval-mode BatchNorm into the convolutions, pad channels for the kernels, upload to HBM. */
 int clasfv_finalize(clasfv_t h);
-/* seg_dev (N,2,T,H,W) logits and motion_dev (N,4,T,H,W) tanh outputs from x_dev (N,3,T,H,W). */
+/* seg_dev (N,2,T,H,W) logits and motion_dev (N,4,T,H,W) tanh outputs from x_dev (N,3,T,H,W).
+   Stream-ordered on `stream` (a hipStream_t; NULL = the default stream), no host synchronisation.
+   The handle keeps one workspace per launch stream (up to 4; a fifth stream takes over the least
+   recently used one after a device synchronisation), so forwards issued on different streams may run
+   concurrently; calls on one handle must come from one host thread at a time. */
 int clasfv_forward(clasfv_t h, const float* x_dev, int N, int T, int H, int W, float* seg_dev,
                    float* motion_dev, void* stream);
-/* Bytes of library workspace currently held (activation arena; grows to the largest N*T*H*W seen). */
+/* Bytes of library workspace currently held (the per-stream activation arenas; each grows to the
+   largest N*T*H*W seen on its stream). */
 int64_t clasfv_workspace_bytes(clasfv_t h);
 /* Compute dtype of the encoder: CLASFV_DTYPE_FP32 (default; exact-fp32 MFMA, the reference's
  * precision) or CLASFV_DTYPE_BF16 (bf16 activations/weights, fp32 accumulation; BASELINE config[4],
