@@ -485,17 +485,28 @@ def c2_measure(args, model, world, rank, dev, lengths, fuse, steps, warmup):
     plans, n_total = D.global_clip_plan(lengths, fuse, args.step)
     lo, hi = D.shard_bounds(n_total, rank, world)
     evs = []
+    # steps in flight as in run_c1 (only without a data exchange: every rank's collectives keep one
+    # order); the exchange events are recorded in the serial kernel-timing pass
+    inflight = max(1, args.inflight) if D.rows_exchanged(D.owner_of_clips(plans, world), world) == 0 else 1
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(inflight - 1)]
+    issued = [0]
 
-    def step():
+    def serial_step(ev=None):
         return D.segment_videos_sharded(videos, model, num_clips=fuse, step=args.step,
                                         fuse_method=args.fuse_method, rank=rank, world=world,
-                                        batch_size=args.batch_size, lengths=lengths, exchange_events=evs)
+                                        batch_size=args.batch_size, lengths=lengths, exchange_events=ev)
 
+    def step():
+        s = streams[issued[0] % len(streams)]
+        issued[0] += 1
+        with torch.cuda.stream(s):
+            return serial_step()
+
+    torch.cuda.synchronize()
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    evs.clear()
-    dt, kt, out = timed(step, steps, 0, eng, world, dev)
+    dt, kt, out = timed(step, steps, 0, eng, world, dev, kt_fn=lambda: serial_step(evs))
     ex_ms = sum(a.elapsed_time(b) for a, b in evs) / steps if evs else 0.0
     t = torch.tensor([ex_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -509,7 +520,7 @@ def c2_measure(args, model, world, rank, dev, lengths, fuse, steps, warmup):
     del videos
     torch.cuda.empty_cache()
     return {"value": round(n_total * steps / dt, 3), "unit": "clips/s", "ms_per_step": round(dt / steps * 1e3, 3),
-            "clips_per_step": n_total, "fuse": fuse, "forward": fwd, "per_rank": per_rank,
+            "clips_per_step": n_total, "fuse": fuse, "steps_in_flight": inflight, "forward": fwd, "per_rank": per_rank,
             "rows_exchanged_per_step": rows, "bytes_exchanged_per_step": nbytes,
             "exchange_ms_per_step": round(float(t.item()), 4),
             "exchange_transfer_ms": round(xfer_ms, 4),
