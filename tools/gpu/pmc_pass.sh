@@ -3,7 +3,7 @@
 # config[1], bf16 config[4] and fp32 config[3] forwards, then the clock / MFMA-busy pass (clock.sh).
 # usage (GPU box): bash tools/gpu/pmc_pass.sh OUTDIR
 out=${1:-gpurun_out/pmc}; mkdir -p $out; export TMPDIR=/tmp
-B="bench.py --steps 2 --warmup 1 --cpu-baseline 0 --extra-bf16 0 --extra-c3 0 --extra-stream 0 --parity-random 0 --extra-c2-ragged 0"
+B="bench.py --steps 2 --warmup 1 --inflight 1 --cpu-baseline 0 --extra-bf16 0 --extra-c3 0 --extra-stream 0 --parity-random 0 --extra-c2-ragged 0"
 for tag in fp32 bf16 fp32_c3; do
   case $tag in fp32) A="$B";; bf16) A="$B --dtype bf16";;
     fp32_c3) A="bench.py --workload c3 --steps 2 --warmup 1 --c3-batch 8";; esac
