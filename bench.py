@@ -347,9 +347,11 @@ def random_recipe_parity(args, model, step, dtype, recipe="random"):
     import clasfv_amd.weights as W
     if not os.path.exists(NORTHSTAR[recipe]):
         return None
+    torch.cuda.synchronize()  # no step in flight reads the weights being replaced
     model.load_state_dict(W.recipe_state_dict(recipe, W.DEFAULT_SEED))
     try:
-        out = step()
+        out = step()  # the one-stream step: its masks are read on this stream
+        torch.cuda.synchronize()
         return northstar_parity(args, out[0], dtype, recipe=recipe) if 0 in out else None
     finally:
         model.load_state_dict(W.recipe_state_dict(BENCH_WEIGHTS, W.DEFAULT_SEED))
@@ -632,8 +634,8 @@ def run_c1(args, model, world, rank, dev):
     fwd = forward_stats(ktimes, (hi - lo) * args.steps, GFLOP_PER_CLIP, peak, args.dtype)
     lv_frac = float(np.mean([o.float().mean().item() for o in out.values()])) if out else 0.0
     parity = northstar_parity(args, out[0], args.dtype) if 0 in out else None
-    parity_random = random_recipe_parity(args, model, step, args.dtype) if world == 1 and args.parity_random else None
-    parity_deep = (random_recipe_parity(args, model, step, args.dtype, "deep")
+    parity_random = random_recipe_parity(args, model, serial_step, args.dtype) if world == 1 and args.parity_random else None
+    parity_deep = (random_recipe_parity(args, model, serial_step, args.dtype, "deep")
                    if world == 1 and args.parity_random else None)
 
     bf16 = None
@@ -648,9 +650,9 @@ def run_c1(args, model, world, rank, dev):
                 "forward": forward_stats(k16, (hi - lo) * args.steps, GFLOP_PER_CLIP, BF16_PEAK_TFLOPS, "bf16"),
                 "dice_delta_vs_fp32_fused_masks": round(float(max(d16)) if d16 else 0.0, 6),
                 "parity_vs_cpu": northstar_parity(args, out16[0], "bf16") if 0 in out16 else None,
-                "parity_vs_cpu_random_weights": (random_recipe_parity(args, model, step, "bf16")
+                "parity_vs_cpu_random_weights": (random_recipe_parity(args, model, serial_step, "bf16")
                                                  if world == 1 and args.parity_random else None),
-                "parity_vs_cpu_deep_weights": (random_recipe_parity(args, model, step, "bf16", "deep")
+                "parity_vs_cpu_deep_weights": (random_recipe_parity(args, model, serial_step, "bf16", "deep")
                                                if world == 1 and args.parity_random else None),
                 "roofline": kernel_roofline(k16, BF16_PEAK_TFLOPS, "bf16"),
                 "kernels": kernel_table(k16, "bf16"),

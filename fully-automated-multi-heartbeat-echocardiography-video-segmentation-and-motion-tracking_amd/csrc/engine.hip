@@ -745,6 +745,8 @@ int clasfv_finalize(clasfv_t h) {
     if (!p.loaded && p.name.find(".fc.") == std::string::npos)
       return fail(CLASFV_ENOTREADY, "parameter not loaded: " + p.name);
   DEVICE_GUARD(h->device);
+  // forwards still in flight on any stream read the weight images replaced below
+  HIP_TRY(hipDeviceSynchronize());
   const bool bf16 = h->dtype == CLASFV_DTYPE_BF16;
   for (auto& c : h->convs) layout_conv(c, bf16);
   for (auto& c : h->proj) layout_conv(c, bf16);

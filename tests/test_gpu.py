@@ -1423,6 +1423,31 @@ def test_config2_ragged_over_8_ranks_exchanges_and_equals_one_rank(echo_model):
 
 
 @pytest.mark.timeout(400)
+def test_bench_c1_line_parity_with_steps_in_flight():
+    """The default bench line at N = 1 keeps two steps in flight, and every parity object it reports --
+    fp32 and bf16, against the echo / random / deep CPU fixtures -- is within its bar (the recipe
+    checks run one-stream steps after a device sync: a step in flight on the other stream once
+    handed its masks to the host before they were written)."""
+    import json
+    import subprocess
+    import sys
+    cmd = [sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--extra-c3", "0", "--extra-stream", "0",
+           "--cpu-baseline", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=380, cwd=REPO, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["config"]["steps_in_flight"] == 2
+    b = line["bf16"]
+    checks = {"fp32": line["parity"], "fp32 random": line["parity_random_weights"], "fp32 deep": line["parity_deep_weights"],
+              "bf16": b["parity_vs_cpu"], "bf16 random": b["parity_vs_cpu_random_weights"],
+              "bf16 deep": b["parity_vs_cpu_deep_weights"]}
+    for name, p in checks.items():
+        assert p is not None and p["within_bar"], (name, p)
+    assert line["parity_deep_weights"]["ed_es_pairs_equal"] and line["parity_deep_weights"]["ef_delta_max_per_systole"] <= 1e-3
+
+
+@pytest.mark.timeout(400)
 @pytest.mark.parametrize("workload", ["c1", "c2", "c2r"])
 def test_bench_self_launches_ranks(workload):
     """`bench.py --gpus 2` without a launcher starts the 2 rank processes itself (here over gloo, both
