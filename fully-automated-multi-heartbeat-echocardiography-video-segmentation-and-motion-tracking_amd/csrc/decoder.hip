@@ -315,9 +315,10 @@ __device__ inline void decoder_heads_bf16(const DecParams& p, const f32x4 (&h1)[
 // (the same operations and order as the packed form, so bit-identical)
 // MODE_ + 16 (LIX, knock-out builds): every wave evaluates its source indices itself (src_index per
 // tap and voxel row / column, the staging windows) instead of reading DecParams::idx; + 32 (bf16
-// engines): W2's pieces split in the kernel (decoder_heads_bf16's W2S). Both bit-identical.
+// engines): W2's pieces split in the kernel (decoder_heads_bf16's W2S). Both bit-identical. + 64
+// (knock-out builds): the fp32 engines' form at five waves per SIMD (96 VGPRs, a few spilled).
 template <int MODE_, int TROWS = 8>
-__global__ __launch_bounds__(32 * TROWS) __attribute__((amdgpu_waves_per_eu((MODE_ & 7) == 4 ? 4 : 5, (MODE_ & 7) == 4 ? 4 : 5))) void decoder_kernel(DecParams p) {
+__global__ __launch_bounds__(32 * TROWS) __attribute__((amdgpu_waves_per_eu(((MODE_ & 7) == 4 && !(MODE_ & 64)) ? 4 : 5, ((MODE_ & 7) == 4 && !(MODE_ & 64)) ? 4 : 5))) void decoder_kernel(DecParams p) {
   constexpr int MODE = MODE_ & 7;
   constexpr bool SC = (MODE_ & 8) != 0;
   constexpr bool LIX = (MODE_ & 16) != 0;
@@ -650,6 +651,7 @@ static hipError_t launch_dec(const DecParams& p, hipStream_t s, int mode, int th
   if (th == 8 && mode == 0 + 16) k = decoder_kernel<0 + 16>;
   if (th == 8 && mode == 1 + 16) k = decoder_kernel<1 + 16>;
   if (th == 8 && mode == 1 + 32) k = decoder_kernel<1 + 32>;
+  if (th == 8 && mode == 4 + 64) k = decoder_kernel<4 + 64>;
 #endif
   if (!k) return hipErrorInvalidValue;
   if (!(mode & 16)) {  // the source-index table this launch reads, filled on the same stream first
@@ -708,13 +710,14 @@ hipError_t launch_decoder(const DecParams& p, hipStream_t s) {
 #ifdef CLASFV_KNOCKOUTS
 // tools/convbench.hip: ko 0 = 8-row tiles; 2, 3 = decoder_kernel's knock-out modes; + 16: 16-row tiles;
 // + 32: single-lane interpolation FMAs; + 64: per-wave index arithmetic (no table); + 128: bf16 W2
-// split in the kernel
+// split in the kernel; + 256: the fp32 engines' decoder at five waves per SIMD
 hipError_t launch_decoder_ko(const DecParams& p, hipStream_t s, int ko) {
   const int m = ko & 15;
   const int base = m == 2 || m == 3 ? m : (p.bf16 ? 1 : p.x3 ? 4 : 0);
   int mode = (ko & 32) && (base == 1 || base == 4) ? base + 8 : base;
   if (ko & 64) mode += 16;
   if ((ko & 128) && base == 1) mode += 32;
+  if ((ko & 256) && base == 4) mode += 64;
   return launch_dec(p, s, mode, (ko & 16) ? 16 : 8);
 }
 #endif
